@@ -1,0 +1,153 @@
+"""ctypes binding of libhip_raytrace.so (include/hip_raytrace.h, include/hrt_host.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` / ``make -C epq_raytracer_amd/csrc``.
+There is no fallback: if the shared object is missing or a call fails, this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int32, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libhip_raytrace.so")
+
+# ---- std430 records (assets/raytracing.glsl:51-153) as numpy dtypes + ctypes structs ----------
+
+MATERIAL_DTYPE = np.dtype([("colour", "<f4", 4), ("emission", "<f4", 4), ("settings", "<f4", 4)])
+RAY_DTYPE = np.dtype([("sample_centre", "<f4", 4)])
+SPHERE_DTYPE = np.dtype([("centre", "<f4", 3), ("radius", "<f4"), ("material", MATERIAL_DTYPE)])
+TRIANGLE_DTYPE = np.dtype([("a", "<f4", 4), ("edge_one", "<f4", 4), ("edge_two", "<f4", 4), ("normal", "<f4", 4)])
+MESH_DTYPE = np.dtype([("min_point", "<f4", 3), ("first_index", "<u4"), ("max_point", "<f4", 3), ("len", "<u4"),
+                       ("material", MATERIAL_DTYPE)])
+assert MATERIAL_DTYPE.itemsize == 48 and RAY_DTYPE.itemsize == 16 and SPHERE_DTYPE.itemsize == 64
+assert TRIANGLE_DTYPE.itemsize == 64 and MESH_DTYPE.itemsize == 80
+
+
+class PushConstants(ctypes.Structure):
+    """raytrace_shader::PushConstants (assets/raytracing.glsl:135-153), 124 bytes."""
+
+    _fields_ = [
+        ("cam_pos", c_float * 4),
+        ("cam_alignment_mat", c_float * 16),
+        ("num_rays", c_int32),
+        ("num_spheres", c_int32),
+        ("num_meshes", c_int32),
+        ("num_samples", c_int32),
+        ("jitter_size", c_float),
+        ("max_bounces", c_int32),
+        ("use_environment_light", c_uint32),
+        ("rng_offset", c_uint32),
+        ("init", c_uint32),
+        ("width", c_uint32),
+        ("height", c_uint32),
+    ]
+
+
+assert ctypes.sizeof(PushConstants) == 124
+
+
+class CreateInfo(ctypes.Structure):
+    _fields_ = [("width", c_uint32), ("height", c_uint32), ("device", c_int32), ("mode", c_uint32),
+                ("row_tile", c_uint32), ("part_index", c_uint32), ("part_count", c_uint32)]
+
+
+class Layout(ctypes.Structure):
+    _fields_ = [("width", c_uint32), ("height", c_uint32), ("local_rows", c_uint32), ("row_tile", c_uint32),
+                ("part_index", c_uint32), ("part_count", c_uint32), ("mode", c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("segments", c_uint64), ("tri_tests", c_uint64), ("traces", c_uint64), ("accumulates", c_uint64),
+                ("last_trace_ms", c_float), ("total_trace_ms", c_float)]
+
+
+HRT_OK = 0
+STATUS_NAMES = {0: "HRT_OK", 1: "HRT_ERR_INVALID_ARGUMENT", 2: "HRT_ERR_NO_DEVICE", 3: "HRT_ERR_OUT_OF_MEMORY",
+                4: "HRT_ERR_NO_SCENE", 5: "HRT_ERR_HIP", 6: "HRT_ERR_IO"}
+MODE_RGBA8, MODE_RGBA32F = 0, 1
+IMG_TRACE, IMG_ACCUM = 0, 1
+FMT_RGBA8, FMT_RGBA32F = 0, 1
+OPT_KERNEL_VARIANT, OPT_COUNTERS = 1, 2
+
+# Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).
+EXPORTED_SYMBOLS = (
+    "hrt_abi_version", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate",
+    "hrt_read_image", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
+    "hrt_stream", "hrt_last_error",
+    "hrt_host_create_rays", "hrt_host_view_matrix", "hrt_host_transform_meshes",
+    "hrt_obj_load", "hrt_obj_num_meshes", "hrt_obj_mesh", "hrt_obj_free",
+)
+
+
+class HrtError(RuntimeError):
+    """A non-OK hrt_status (the reference would have panicked in .unwrap())."""
+
+    def __init__(self, status: int, where: str, detail: str = ""):
+        self.status = status
+        super().__init__(f"{where} failed: {STATUS_NAMES.get(status, status)}{': ' + detail if detail else ''}")
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libhip_raytrace.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                           " or `make -C epq_raytracer_amd/csrc` (no CPU fallback exists)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P = c_void_p
+    sig = {
+        "hrt_abi_version": (c_uint32, []),
+        "hrt_create": (c_int32, [POINTER(CreateInfo), POINTER(c_void_p)]),
+        "hrt_destroy": (None, [P]),
+        "hrt_set_scene": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32]),
+        "hrt_trace": (c_int32, [P, POINTER(PushConstants)]),
+        "hrt_accumulate": (c_int32, [P, c_uint32]),
+        "hrt_read_image": (c_int32, [P, c_uint32, c_uint32, P, c_size_t]),
+        "hrt_get_layout": (c_int32, [P, POINTER(Layout)]),
+        "hrt_synchronize": (c_int32, [P]),
+        "hrt_get_stats": (c_int32, [P, POINTER(Stats)]),
+        "hrt_reset_stats": (c_int32, [P]),
+        "hrt_set_option": (c_int32, [P, c_uint32, c_int64]),
+        "hrt_stream": (c_void_p, [P]),
+        "hrt_last_error": (c_char_p, [P]),
+        "hrt_host_create_rays": (c_uint32, [c_uint32, c_uint32, c_float, c_float, POINTER(c_float), P,
+                                            POINTER(c_float)]),
+        "hrt_host_view_matrix": (None, [POINTER(c_float), POINTER(c_float), POINTER(c_float)]),
+        "hrt_host_transform_meshes": (c_int32, [c_uint32, P, P, P, P, P, P, c_uint32, P]),
+        "hrt_obj_load": (c_int32, [c_char_p, POINTER(c_void_p)]),
+        "hrt_obj_num_meshes": (c_uint32, [P]),
+        "hrt_obj_mesh": (c_int32, [P, c_uint32, POINTER(c_char_p), POINTER(c_void_p), POINTER(c_uint32),
+                                   POINTER(c_void_p), POINTER(c_uint32)]),
+        "hrt_obj_free": (None, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, where: str, ctx=None) -> None:
+    if status != HRT_OK:
+        detail = load().hrt_last_error(ctx)
+        raise HrtError(status, where, detail.decode() if detail else "")
+
+
+def ptr(a: np.ndarray | None) -> c_void_p:
+    if a is None or a.size == 0:
+        return c_void_p(0)
+    assert a.flags["C_CONTIGUOUS"]
+    return c_void_p(a.ctypes.data)
+
+
+def f3(v) -> ctypes.Array:
+    return (c_float * 3)(*[float(np.float32(x)) for x in v])

@@ -1,0 +1,427 @@
+// hrt_api.cpp -- the C ABI of libhip_raytrace.so (include/hip_raytrace.h).
+//
+// A context owns everything the reference's RayTracePipeline + DiffusePipeline own on the Vulkan
+// side (src/raytrace_pipeline.rs:31-46, src/diffuse.rs:22-30): the scene buffers, the trace image,
+// the accumulated image, the queue (here: one HIP stream) -- plus the device counters and timing
+// events that the reference does not have.  Memory is allocated once per context; hrt_trace and
+// hrt_accumulate only enqueue kernels (no allocation, no host sync), so a caller may capture them.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "hip_raytrace.h"
+#include "hrt_kernels.h"
+
+static_assert(sizeof(hrt_material) == 48, "std430 RayTracingMaterial");
+static_assert(sizeof(hrt_ray) == 16, "std430 Ray");
+static_assert(sizeof(hrt_sphere) == 64, "std430 Sphere");
+static_assert(sizeof(hrt_triangle) == 64, "std430 Triangle");
+static_assert(sizeof(hrt_mesh) == 80, "std430 Mesh");
+static_assert(sizeof(hrt_push_constants) == 124, "push constant block (src/raytrace_pipeline.rs:125-139)");
+static_assert(offsetof(hrt_push_constants, num_rays) == 80, "push layout");
+static_assert(offsetof(hrt_push_constants, height) == 120, "push layout");
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct EventPair {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+
+}  // namespace
+
+struct hrt_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t width = 0, height = 0, mode = HRT_MODE_RGBA8;
+  uint32_t row_tile = 0, part_index = 0, part_count = 1, local_rows = 0;
+
+  float4* rays = nullptr;
+  hrt_sphere* spheres = nullptr;
+  hrt_triangle* tris = nullptr;
+  hrt_mesh* meshes = nullptr;
+  uint32_t n_rays = 0, n_spheres = 0, n_tris = 0, n_meshes = 0;
+  bool scene_set = false;
+
+  uint32_t* trace8 = nullptr;
+  uint32_t* accum8 = nullptr;
+  float4* trace32 = nullptr;
+  float4* accum32 = nullptr;
+  void* scratch = nullptr;  // format conversion for hrt_read_image
+  unsigned long long* counters = nullptr;
+
+  int variant = 0;
+  bool counters_on = true;
+
+  std::vector<EventPair> event_pool;     // reusable
+  std::vector<EventPair> pending;        // recorded, not yet harvested
+  uint64_t traces = 0, accumulates = 0;
+  float last_ms = 0.0f, total_ms = 0.0f;
+
+  std::string err;
+
+  size_t npix() const { return (size_t)local_rows * width; }
+};
+
+namespace {
+
+hrt_status fail(hrt_context* ctx, hrt_status st, const std::string& msg) {
+  if (ctx)
+    ctx->err = msg;
+  else
+    g_create_error = msg;
+  return st;
+}
+
+hrt_status hip_fail(hrt_context* ctx, hipError_t e, const char* what) {
+  std::string msg = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+  return fail(ctx, e == hipErrorOutOfMemory ? HRT_ERR_OUT_OF_MEMORY : HRT_ERR_HIP, msg);
+}
+
+#define HRT_HIP(ctx, call)                                      \
+  do {                                                          \
+    hipError_t e_ = (call);                                     \
+    if (e_ != hipSuccess) return hip_fail((ctx), e_, #call);    \
+  } while (0)
+
+// Make the context's device current for the calling thread (contexts may live on any device).
+hrt_status bind(hrt_context* ctx) {
+  HRT_HIP(ctx, hipSetDevice(ctx->device));
+  return HRT_OK;
+}
+
+template <typename T>
+void free_dev(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+hrt_status harvest_events(hrt_context* ctx) {
+  for (auto& ev : ctx->pending) {
+    HRT_HIP(ctx, hipEventSynchronize(ev.stop));
+    float ms = 0.0f;
+    HRT_HIP(ctx, hipEventElapsedTime(&ms, ev.start, ev.stop));
+    ctx->last_ms = ms;
+    ctx->total_ms += ms;
+    ctx->event_pool.push_back(ev);
+  }
+  ctx->pending.clear();
+  return HRT_OK;
+}
+
+}  // namespace
+
+extern "C" uint32_t hrt_abi_version(void) { return HRT_ABI_VERSION; }
+
+extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_ctx) {
+  g_create_error.clear();
+  if (!info || !out_ctx) return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_create: null argument");
+  *out_ctx = nullptr;
+  if (info->mode != HRT_MODE_RGBA8 && info->mode != HRT_MODE_RGBA32F)
+    return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_create: unknown mode");
+  if (info->width == 0 || info->height == 0)
+    return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_create: zero image size");
+  if ((uint64_t)info->width * info->height > (1ull << 31))
+    return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_create: image larger than 2^31 pixels");
+  const uint32_t parts = info->part_count == 0 ? 1 : info->part_count;
+  if (parts > 1 && (info->row_tile == 0 || info->part_index >= parts))
+    return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_create: bad row-tile partition");
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(nullptr, HRT_ERR_NO_DEVICE, "hrt_create: no HIP device visible");
+  int dev = info->device;
+  if (dev < 0) {
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  }
+  if (dev >= ndev) return fail(nullptr, HRT_ERR_NO_DEVICE, "hrt_create: device ordinal out of range");
+
+  auto* ctx = new hrt_context();
+  ctx->device = dev;
+  ctx->width = info->width;
+  ctx->height = info->height;
+  ctx->mode = info->mode;
+  ctx->part_count = parts;
+  if (parts > 1) {
+    ctx->row_tile = info->row_tile;
+    ctx->part_index = info->part_index;
+    const uint32_t tiles = (info->height + info->row_tile - 1) / info->row_tile;
+    const uint32_t tiles_per_part = (tiles + parts - 1) / parts;
+    ctx->local_rows = tiles_per_part * info->row_tile;
+  } else {
+    ctx->row_tile = info->height;
+    ctx->part_index = 0;
+    ctx->local_rows = info->height;
+  }
+
+  auto bail = [&](hrt_status st) {
+    std::string msg = ctx->err;
+    hrt_destroy(ctx);
+    return fail(nullptr, st, msg);
+  };
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return bail(st);
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamCreate"));
+  const size_t np = ctx->npix();
+  if (ctx->mode == HRT_MODE_RGBA8) {
+    if ((e = hipMalloc((void**)&ctx->trace8, np * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(trace)"));
+    if ((e = hipMalloc((void**)&ctx->accum8, np * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(accum)"));
+  } else {
+    if ((e = hipMalloc((void**)&ctx->trace32, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(trace)"));
+    if ((e = hipMalloc((void**)&ctx->accum32, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(accum)"));
+  }
+  if ((e = hipMalloc(&ctx->scratch, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(scratch)"));
+  if ((e = hipMalloc((void**)&ctx->counters, 2 * sizeof(unsigned long long))) != hipSuccess)
+    return bail(hip_fail(ctx, e, "hipMalloc(counters)"));
+  if ((e = hipMemsetAsync(ctx->counters, 0, 2 * sizeof(unsigned long long), ctx->stream)) != hipSuccess)
+    return bail(hip_fail(ctx, e, "hipMemset(counters)"));
+  // Fresh images read as the cleared state (0,0,0,1) until the first dispatch writes them.
+  if ((e = hrt::launch_clear(ctx->trace8, ctx->trace32, np, ctx->stream)) != hipSuccess)
+    return bail(hip_fail(ctx, e, "clear"));
+  if ((e = hrt::launch_clear(ctx->accum8, ctx->accum32, np, ctx->stream)) != hipSuccess)
+    return bail(hip_fail(ctx, e, "clear"));
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
+  *out_ctx = ctx;
+  return HRT_OK;
+}
+
+extern "C" void hrt_destroy(hrt_context* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  free_dev(ctx->rays);
+  free_dev(ctx->spheres);
+  free_dev(ctx->tris);
+  free_dev(ctx->meshes);
+  free_dev(ctx->trace8);
+  free_dev(ctx->accum8);
+  free_dev(ctx->trace32);
+  free_dev(ctx->accum32);
+  free_dev(ctx->scratch);
+  free_dev(ctx->counters);
+  for (auto& ev : ctx->event_pool) {
+    (void)hipEventDestroy(ev.start);
+    (void)hipEventDestroy(ev.stop);
+  }
+  for (auto& ev : ctx->pending) {
+    (void)hipEventDestroy(ev.start);
+    (void)hipEventDestroy(ev.stop);
+  }
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+namespace {
+
+template <typename T>
+hrt_status upload(hrt_context* ctx, T*& dst, const T* src, uint32_t n, const char* what) {
+  free_dev(dst);
+  const size_t bytes = (size_t)(n ? n : 1) * sizeof(T);  // keep a valid pointer for empty lists
+  HRT_HIP(ctx, hipMalloc((void**)&dst, bytes));
+  if (n) HRT_HIP(ctx, hipMemcpyAsync(dst, src, (size_t)n * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  (void)what;
+  return HRT_OK;
+}
+
+}  // namespace
+
+extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint32_t n_rays, const hrt_sphere* spheres,
+                                    uint32_t n_spheres, const hrt_triangle* tris, uint32_t n_tris,
+                                    const hrt_mesh* meshes, uint32_t n_meshes) {
+  if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
+  if ((uint64_t)n_rays != (uint64_t)ctx->width * ctx->height || !rays)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_set_scene: need width*height rays");
+  if ((n_spheres && !spheres) || (n_tris && !tris) || (n_meshes && !meshes))
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_set_scene: null record array with nonzero count");
+  for (uint32_t m = 0; m < n_meshes; ++m) {
+    if ((uint64_t)meshes[m].first_index + meshes[m].len > n_tris)
+      return fail(ctx, HRT_ERR_INVALID_ARGUMENT,
+                  "hrt_set_scene: mesh " + std::to_string(m) + " triangle range exceeds the triangle buffer");
+  }
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  static_assert(sizeof(float4) == sizeof(hrt_ray), "ray record");
+  if ((st = upload(ctx, ctx->rays, reinterpret_cast<const float4*>(rays), n_rays, "rays")) != HRT_OK) return st;
+  if ((st = upload(ctx, ctx->spheres, spheres, n_spheres, "spheres")) != HRT_OK) return st;
+  if ((st = upload(ctx, ctx->tris, tris, n_tris, "triangles")) != HRT_OK) return st;
+  if ((st = upload(ctx, ctx->meshes, meshes, n_meshes, "meshes")) != HRT_OK) return st;
+  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
+  ctx->n_rays = n_rays;
+  ctx->n_spheres = n_spheres;
+  ctx->n_tris = n_tris;
+  ctx->n_meshes = n_meshes;
+  ctx->scene_set = true;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) {
+  if (!ctx || !pc) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  if (pc->init) {  // RayTracePipeline::init, src/raytrace_pipeline.rs:190-213
+    HRT_HIP(ctx, hrt::launch_clear(ctx->trace8, ctx->trace32, ctx->npix(), ctx->stream));
+    return HRT_OK;
+  }
+  if (!ctx->scene_set) return fail(ctx, HRT_ERR_NO_SCENE, "hrt_trace: hrt_set_scene has not been called");
+  if (pc->width != ctx->width || pc->height != ctx->height)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_trace: push constant width/height differ from the context");
+  if (pc->num_spheres < 0 || (uint32_t)pc->num_spheres > ctx->n_spheres || pc->num_meshes < 0 ||
+      (uint32_t)pc->num_meshes > ctx->n_meshes)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_trace: num_spheres/num_meshes exceed the uploaded scene");
+
+  hrt::TraceParams p{};
+  p.rays = ctx->rays;
+  p.spheres = ctx->spheres;
+  p.tris = ctx->tris;
+  p.meshes = ctx->meshes;
+  p.img8 = ctx->trace8;
+  p.img32 = ctx->trace32;
+  p.counters = ctx->counters_on ? ctx->counters : nullptr;
+  p.pc = *pc;
+  p.local_rows = ctx->local_rows;
+  p.row_tile = ctx->row_tile;
+  p.part_index = ctx->part_index;
+  p.part_count = ctx->part_count;
+  // The fused-loop variant assumes max_bounces >= 0 (a negative count traces no segment at all).
+  const int variant = pc->max_bounces < 0 ? 1 : ctx->variant;
+
+  EventPair ev;
+  if (!ctx->event_pool.empty()) {
+    ev = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+  } else {
+    HRT_HIP(ctx, hipEventCreate(&ev.start));
+    HRT_HIP(ctx, hipEventCreate(&ev.stop));
+  }
+  HRT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
+  hipError_t e = hrt::launch_trace(p, variant, ctx->stream);
+  if (e != hipSuccess) {
+    ctx->event_pool.push_back(ev);
+    return hip_fail(ctx, e, "trace kernel launch");
+  }
+  HRT_HIP(ctx, hipEventRecord(ev.stop, ctx->stream));
+  ctx->pending.push_back(ev);
+  ctx->traces++;
+  if (ctx->pending.size() > 256) return harvest_events(ctx);  // bound the pending list
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_accumulate(hrt_context* ctx, uint32_t frame) {
+  if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  HRT_HIP(ctx, hrt::launch_accumulate(ctx->accum8, ctx->trace8, ctx->accum32, ctx->trace32, ctx->npix(), frame,
+                                      ctx->stream));
+  ctx->accumulates++;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes) {
+  if (!ctx || !dst) return HRT_ERR_INVALID_ARGUMENT;
+  if (image_id != HRT_IMG_TRACE && image_id != HRT_IMG_ACCUM)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown image id");
+  if (fmt != HRT_FMT_RGBA8 && fmt != HRT_FMT_RGBA32F)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown format");
+  const size_t np = ctx->npix();
+  const size_t need = np * (fmt == HRT_FMT_RGBA8 ? 4 : 16);
+  if (bytes < need) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: destination too small");
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  const bool accum = image_id == HRT_IMG_ACCUM;
+  const void* src = nullptr;
+  if (ctx->mode == HRT_MODE_RGBA8) {
+    const uint32_t* s8 = accum ? ctx->accum8 : ctx->trace8;
+    if (fmt == HRT_FMT_RGBA8) {
+      src = s8;
+    } else {
+      HRT_HIP(ctx, hrt::launch_convert(s8, (float4*)ctx->scratch, nullptr, nullptr, np, ctx->stream));
+      src = ctx->scratch;
+    }
+  } else {
+    const float4* s32 = accum ? ctx->accum32 : ctx->trace32;
+    if (fmt == HRT_FMT_RGBA32F) {
+      src = s32;
+    } else {
+      HRT_HIP(ctx, hrt::launch_convert(nullptr, nullptr, s32, (uint32_t*)ctx->scratch, np, ctx->stream));
+      src = ctx->scratch;
+    }
+  }
+  HRT_HIP(ctx, hipMemcpyAsync(dst, src, need, hipMemcpyDefault, ctx->stream));
+  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_get_layout(const hrt_context* ctx, hrt_layout* out) {
+  if (!ctx || !out) return HRT_ERR_INVALID_ARGUMENT;
+  out->width = ctx->width;
+  out->height = ctx->height;
+  out->local_rows = ctx->local_rows;
+  out->row_tile = ctx->row_tile;
+  out->part_index = ctx->part_index;
+  out->part_count = ctx->part_count;
+  out->mode = ctx->mode;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_synchronize(hrt_context* ctx) {
+  if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out) {
+  if (!ctx || !out) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = hrt_synchronize(ctx);
+  if (st != HRT_OK) return st;
+  if ((st = harvest_events(ctx)) != HRT_OK) return st;
+  unsigned long long c[2] = {0, 0};
+  HRT_HIP(ctx, hipMemcpy(c, ctx->counters, sizeof c, hipMemcpyDeviceToHost));
+  out->segments = c[0];
+  out->tri_tests = c[1];
+  out->traces = ctx->traces;
+  out->accumulates = ctx->accumulates;
+  out->last_trace_ms = ctx->last_ms;
+  out->total_trace_ms = ctx->total_ms;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_reset_stats(hrt_context* ctx) {
+  if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = hrt_synchronize(ctx);
+  if (st != HRT_OK) return st;
+  if ((st = harvest_events(ctx)) != HRT_OK) return st;
+  HRT_HIP(ctx, hipMemsetAsync(ctx->counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
+  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->traces = ctx->accumulates = 0;
+  ctx->last_ms = ctx->total_ms = 0.0f;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value) {
+  if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
+  switch (key) {
+    case HRT_OPT_KERNEL_VARIANT:
+      if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be 0 or 1");
+      ctx->variant = (int)value;
+      return HRT_OK;
+    case HRT_OPT_COUNTERS:
+      ctx->counters_on = value != 0;
+      return HRT_OK;
+    default:
+      return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "unknown option key");
+  }
+}
+
+extern "C" void* hrt_stream(hrt_context* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+extern "C" const char* hrt_last_error(const hrt_context* ctx) {
+  return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}

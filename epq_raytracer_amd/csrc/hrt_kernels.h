@@ -1,0 +1,31 @@
+// hrt_kernels.h -- launch interface between the C-ABI layer (hrt_api.cpp) and the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hip_raytrace.h"
+
+namespace hrt {
+
+// Kernel argument block (passed by value; lives in the kernarg segment, read through SGPRs).
+struct TraceParams {
+  const float4* rays;            // W*H sample centres, indexed by global pixel id
+  const hrt_sphere* spheres;
+  const hrt_triangle* tris;
+  const hrt_mesh* meshes;
+  uint32_t* img8;                // local_rows x W packed RGBA8 (RGBA8 mode) or nullptr
+  float4* img32;                 // local_rows x W float4 (RGBA32F mode) or nullptr
+  unsigned long long* counters;  // [0] segments, [1] triangle tests; nullptr = off
+  hrt_push_constants pc;
+  uint32_t local_rows, row_tile, part_index, part_count;
+};
+
+hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream);
+hipError_t launch_clear(uint32_t* img8, float4* img32, size_t npix, hipStream_t stream);
+hipError_t launch_accumulate(uint32_t* cur8, const uint32_t* new8, float4* cur32, const float4* new32, size_t npix,
+                             uint32_t frame, hipStream_t stream);
+hipError_t launch_convert(const uint32_t* src8, float4* dst32, const float4* src32, uint32_t* dst8, size_t npix,
+                          hipStream_t stream);
+
+}  // namespace hrt

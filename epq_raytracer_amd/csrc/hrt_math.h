@@ -1,0 +1,168 @@
+// hrt_math.h -- device-side numerics for the gfx950 path tracer.
+//
+// The GLSL reference (assets/raytracing.glsl) leaves dot/cross summation order, FMA contraction,
+// normalize's form and the transcendental algorithms to the Vulkan driver.  This header pins each
+// of them (DESIGN.md "numerics spec" S1-S7) so that a frame is reproducible bit for bit on any IEEE
+// binary32 machine; the CPU oracle (oracle/rt_oracle.c) restates the same spec independently.
+// The file is compiled with -ffp-contract=off: every fma below is explicit, nothing else fuses.
+// gfx950's f32 '/', sqrt, fma, u32->f32 and rint are correctly rounded with denormals kept
+// (measured bit-exact against the host over 4M inputs, tools/probe/probe.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hrt {
+
+constexpr float kFltMax = 3.402823466e+38f;  // raytracing.glsl:2
+
+struct f3 {
+  float x, y, z;
+};
+
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return {x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ f3 adds(f3 a, float s) { return {a.x + s, a.y + s, a.z + s}; }
+
+// S2: dot / cross / mat3*vec with explicit FMA in a fixed order.
+__device__ __forceinline__ float dot(f3 a, f3 b) {
+  return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
+}
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+  return {__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+          __builtin_fmaf(a.x, b.y, -(a.y * b.x))};
+}
+// S4: normalize = v / sqrt(dot(v, v)), correctly rounded divides.
+__device__ __forceinline__ f3 normalize(f3 a) {
+  const float l = __builtin_sqrtf(dot(a, a));
+  return a / l;
+}
+// S6: GLSL 4.60 definitions.
+__device__ __forceinline__ float gmin(float x, float y) { return (y < x) ? y : x; }
+__device__ __forceinline__ float gmax(float x, float y) { return (x < y) ? y : x; }
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// S5: natural log.  m in [sqrt(1/2), sqrt(2)), log(1+f) = f - f^2/2 + f^3 P(f), ln2 split in two.
+__device__ __forceinline__ float spec_log(float x) {
+  uint32_t ix = fbits(x);
+  if (x != x) return x;
+  if (x == 0.0f) return -__builtin_inff();
+  if (ix >> 31) return bitsf(0x7fc00000u);
+  if (ix == 0x7f800000u) return x;
+  int k = 0;
+  if (ix < 0x00800000u) {
+    x = x * 8388608.0f;
+    ix = fbits(x);
+    k = -23;
+  }
+  ix += 0x3f800000u - 0x3f3504f3u;
+  k += (int)(ix >> 23) - 0x7f;
+  ix = (ix & 0x007fffffu) + 0x3f3504f3u;
+  const float f = bitsf(ix) - 1.0f;
+  const float z = f * f;
+  float p = 7.0376836292e-2f;
+  p = __builtin_fmaf(p, f, -1.1514610310e-1f);
+  p = __builtin_fmaf(p, f, 1.1676998740e-1f);
+  p = __builtin_fmaf(p, f, -1.2420140846e-1f);
+  p = __builtin_fmaf(p, f, 1.4249322787e-1f);
+  p = __builtin_fmaf(p, f, -1.6668057665e-1f);
+  p = __builtin_fmaf(p, f, 2.0000714765e-1f);
+  p = __builtin_fmaf(p, f, -2.4999993993e-1f);
+  p = __builtin_fmaf(p, f, 3.3333331174e-1f);
+  float y = (p * f) * z;
+  const float fk = (float)k;
+  y = __builtin_fmaf(fk, -2.12194440e-4f, y);
+  y = __builtin_fmaf(z, -0.5f, y);
+  const float r = f + y;
+  return __builtin_fmaf(fk, 0.693359375f, r);
+}
+
+// S5: sin / cos.  Cody-Waite reduction by pi/2 (3 parts), odd/even polynomials on |r| <= pi/4.
+__device__ __forceinline__ float spec_reduce(float x, int& q) {
+  const float j = __builtin_rintf(x * 0.636619772367581343f);
+  q = (int)j;
+  float r = __builtin_fmaf(-j, 1.5703125f, x);
+  r = __builtin_fmaf(-j, 4.837512969970703125e-4f, r);
+  r = __builtin_fmaf(-j, 7.549789954891882e-8f, r);
+  return r;
+}
+__device__ __forceinline__ float sin_poly(float r) {
+  const float z = r * r;
+  float p = -1.9515295891e-4f;
+  p = __builtin_fmaf(p, z, 8.3321608736e-3f);
+  p = __builtin_fmaf(p, z, -1.6666654611e-1f);
+  return __builtin_fmaf(p * z, r, r);
+}
+__device__ __forceinline__ float cos_poly(float r) {
+  const float z = r * r;
+  float p = 2.443315711809948e-5f;
+  p = __builtin_fmaf(p, z, -1.388731625493765e-3f);
+  p = __builtin_fmaf(p, z, 4.166664568298827e-2f);
+  return __builtin_fmaf(p * z, z, __builtin_fmaf(z, -0.5f, 1.0f));
+}
+// sin and cos of the same argument (both quadrants from one reduction).
+__device__ __forceinline__ void spec_sincos(float x, float& s, float& c) {
+  if (!(__builtin_fabsf(x) <= 1.0e5f)) {
+    const float nan = (x != x) ? x : bitsf(0x7fc00000u);
+    s = nan;
+    c = nan;
+    return;
+  }
+  int q;
+  const float r = spec_reduce(x, q);
+  const float ps = sin_poly(r), pc = cos_poly(r);
+  switch (q & 3) {
+    case 0: s = ps; c = pc; break;
+    case 1: s = pc; c = -ps; break;
+    case 2: s = -ps; c = -pc; break;
+    default: s = -pc; c = ps; break;
+  }
+}
+__device__ __forceinline__ float spec_cos(float x) {
+  float s, c;
+  spec_sincos(x, s, c);
+  return c;
+}
+
+// ---- RNG: assets/raytracing.glsl:13-40 ------------------------------------------------------
+__device__ __forceinline__ uint32_t hash(uint32_t& state) {  // :13-21
+  uint32_t s = state;
+  s ^= 2747636419u;
+  s *= 2654435769u;
+  s ^= s >> 16;
+  s *= 2654435769u;
+  s ^= s >> 16;
+  s *= 2654435769u;
+  state = s;
+  return s;
+}
+// scaleToRange01 :23-25 -- float(4294967295.0) == 2^32, so the divide is an exact power-of-two scale.
+__device__ __forceinline__ float u01(uint32_t s) { return (float)s * 2.3283064365386963e-10f; }
+
+__device__ __forceinline__ float normal_dist(uint32_t& state) {  // :28-33
+  const float theta = 6.2831852f * u01(hash(state));  // 2 * 3.1415926 folded exactly
+  const float rho = __builtin_sqrtf(-2.0f * spec_log(u01(hash(state))));
+  return rho * spec_cos(theta);
+}
+__device__ __forceinline__ f3 unit_sphere(uint32_t& state) {  // :35-40
+  const float x = normal_dist(state);
+  const float y = normal_dist(state);
+  const float z = normal_dist(state);
+  return normalize(mk(x, y, z));
+}
+
+// S7: R8G8B8A8_UNORM store / load.
+__device__ __forceinline__ uint32_t unorm8(float x) {
+  if (!(x > 0.0f)) return 0u;
+  if (x >= 1.0f) return 255u;
+  return (uint32_t)(int)__builtin_rintf(x * 255.0f);
+}
+__device__ __forceinline__ float unorm8_to_float(uint32_t k) { return (float)k / 255.0f; }
+
+}  // namespace hrt

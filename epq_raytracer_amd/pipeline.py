@@ -1,0 +1,246 @@
+"""Host side of the path: the Python mirror of RayTracePipeline (src/raytrace_pipeline.rs) and
+DiffusePipeline (src/diffuse.rs) on top of the C ABI.  Host prep arithmetic (ray centres, view
+matrix, mesh flattening) runs in the native library (hrt_host_*), the dispatches on the GPU.
+
+Mapping to the reference:
+  RayTracerSettings        src/raytracing_app.rs:17-29
+  RayTracePipeline.__init__ src/raytrace_pipeline.rs:51-97   (-> hrt_create + hrt_set_scene)
+  RayTracePipeline.compute  src/raytrace_pipeline.rs:162-187 (-> hrt_trace, init = 0)
+  RayTracePipeline.init     src/raytrace_pipeline.rs:190-213 (-> hrt_trace, init = 1)
+  RayTracePipeline.push_constants  dispatch :216-266 (124-byte block :243-257)
+  DiffusePipeline.next_frame       src/diffuse.rs:73-101 (-> hrt_accumulate)
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from .scene import Camera, RayTracingMesh, Sphere, as_material, get_null_mesh, get_null_sphere
+
+
+@dataclass
+class RayTracerSettings:
+    """src/raytracing_app.rs:17-29."""
+    num_samples: int
+    max_bounces: int
+    use_environment_lighting: bool
+    sample_jitter: Optional[float] = None
+    sphere_data: List[Sphere] = field(default_factory=list)
+    mesh_data: List[RayTracingMesh] = field(default_factory=list)
+    camera_focal_length: float = 1.0
+    viewport_height: float = 2.0
+    up: Sequence[float] = (0.0, 1.0, 0.0)
+
+
+# ---- host prep (native) ---------------------------------------------------------------------
+
+def create_rays(image_size, camera_focal_length, viewport_height, up):
+    """create_ray_subbuffer, src/raytrace_pipeline.rs:289-338 -> (rays[W*H], num_rays, default_jitter)."""
+    lib = _lib.load()
+    w, h = int(image_size[0]), int(image_size[1])
+    rays = np.zeros(max(w * h, 1), dtype=_lib.RAY_DTYPE)
+    jit = ctypes.c_float()
+    n = lib.hrt_host_create_rays(w, h, float(np.float32(camera_focal_length)), float(np.float32(viewport_height)),
+                                 _lib.f3(up), _lib.ptr(rays), ctypes.byref(jit))
+    return rays, int(n), float(jit.value)
+
+
+def view_matrix(direction, up) -> np.ndarray:
+    """get_view_matrix, src/raytrace_pipeline.rs:269-285 -> column-major mat4 as float32[16]."""
+    lib = _lib.load()
+    out = (ctypes.c_float * 16)()
+    lib.hrt_host_view_matrix(_lib.f3(direction), _lib.f3(up), out)
+    return np.frombuffer(out, dtype=np.float32).copy()
+
+
+def transform_meshes(meshes: List[RayTracingMesh]):
+    """transform_meshes, src/raytrace_pipeline.rs:377-428 -> (triangles, mesh records)."""
+    lib = _lib.load()
+    n = len(meshes)
+    pos = [np.ascontiguousarray(m.mesh.positions, np.float32) for m in meshes]
+    idx = [np.ascontiguousarray(m.mesh.indices, np.uint32) for m in meshes]
+    mats = np.array([as_material(m.material) for m in meshes], dtype=_lib.MATERIAL_DTYPE)
+    ntri = sum(int(i.size) // 3 for i in idx)
+    tris = np.zeros(max(ntri, 1), dtype=_lib.TRIANGLE_DTYPE)
+    recs = np.zeros(max(n, 1), dtype=_lib.MESH_DTYPE)
+    pos_ptrs = (ctypes.c_void_p * n)(*[p.ctypes.data for p in pos])
+    idx_ptrs = (ctypes.c_void_p * n)(*[i.ctypes.data if i.size else 0 for i in idx])
+    nv = (ctypes.c_uint32 * n)(*[p.shape[0] for p in pos])
+    ni = (ctypes.c_uint32 * n)(*[i.size for i in idx])
+    st = lib.hrt_host_transform_meshes(n, pos_ptrs, nv, idx_ptrs, ni, _lib.ptr(mats), _lib.ptr(tris), ntri,
+                                       _lib.ptr(recs))
+    _lib.check(st, "hrt_host_transform_meshes")
+    return tris[:ntri], recs[:n]
+
+
+def sphere_records(spheres: List[Sphere]) -> np.ndarray:
+    """create_sphere_subbuffer, src/raytrace_pipeline.rs:342-360."""
+    if not spheres:
+        return np.zeros(0, dtype=_lib.SPHERE_DTYPE)
+    return np.array([s.record() for s in spheres], dtype=_lib.SPHERE_DTYPE)
+
+
+# ---- the device context (one hrt_context = the trace image + the accumulated image) ------------
+
+class HrtContext:
+    """Owner of one hrt_context.  ``partition`` = (row_tile, part_index, part_count) selects the
+    interleaved row tiles this context renders (multi-GPU)."""
+
+    def __init__(self, image_size, device: int = -1, mode: int = _lib.MODE_RGBA8, partition=None):
+        self.lib = _lib.load()
+        info = _lib.CreateInfo()
+        info.width, info.height = int(image_size[0]), int(image_size[1])
+        info.device = int(device)
+        info.mode = int(mode)
+        if partition is not None:
+            info.row_tile, info.part_index, info.part_count = (int(v) for v in partition)
+        else:
+            info.row_tile, info.part_index, info.part_count = 0, 0, 1
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.hrt_create(ctypes.byref(info), ctypes.byref(h)), "hrt_create")
+        self.handle = h
+        lay = _lib.Layout()
+        _lib.check(self.lib.hrt_get_layout(self.handle, ctypes.byref(lay)), "hrt_get_layout", self.handle)
+        self.width, self.height = lay.width, lay.height
+        self.local_rows, self.row_tile = lay.local_rows, lay.row_tile
+        self.part_index, self.part_count, self.mode = lay.part_index, lay.part_count, lay.mode
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.hrt_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st, where):
+        _lib.check(st, where, self.handle)
+
+    def set_scene(self, rays, spheres, tris, meshes):
+        self._check(self.lib.hrt_set_scene(self.handle, _lib.ptr(rays), len(rays), _lib.ptr(spheres), len(spheres),
+                                           _lib.ptr(tris), len(tris), _lib.ptr(meshes), len(meshes)),
+                    "hrt_set_scene")
+
+    def trace(self, pc: _lib.PushConstants):
+        self._check(self.lib.hrt_trace(self.handle, ctypes.byref(pc)), "hrt_trace")
+
+    def accumulate(self, frame: int):
+        self._check(self.lib.hrt_accumulate(self.handle, int(frame) & 0xFFFFFFFF), "hrt_accumulate")
+
+    def synchronize(self):
+        self._check(self.lib.hrt_synchronize(self.handle), "hrt_synchronize")
+
+    def set_option(self, key: int, value: int):
+        self._check(self.lib.hrt_set_option(self.handle, key, value), "hrt_set_option")
+
+    def stats(self) -> _lib.Stats:
+        s = _lib.Stats()
+        self._check(self.lib.hrt_get_stats(self.handle, ctypes.byref(s)), "hrt_get_stats")
+        return s
+
+    def reset_stats(self):
+        self._check(self.lib.hrt_reset_stats(self.handle), "hrt_reset_stats")
+
+    def read(self, image_id: int, fmt: int = _lib.FMT_RGBA8) -> np.ndarray:
+        """Local rows of an image: uint8 (local_rows, W, 4) or float32 (local_rows, W, 4)."""
+        dt = np.uint8 if fmt == _lib.FMT_RGBA8 else np.float32
+        out = np.empty((self.local_rows, self.width, 4), dtype=dt)
+        self._check(self.lib.hrt_read_image(self.handle, image_id, fmt, _lib.ptr(out), out.nbytes), "hrt_read_image")
+        return out
+
+    def read_into(self, image_id: int, fmt: int, dst_ptr: int, nbytes: int):
+        """Copy into caller memory (host or device pointer, e.g. a torch tensor's data_ptr())."""
+        self._check(self.lib.hrt_read_image(self.handle, image_id, fmt, ctypes.c_void_p(dst_ptr), nbytes),
+                    "hrt_read_image")
+
+    def global_rows(self) -> np.ndarray:
+        """Global row index of each local row (rows >= height are padding)."""
+        lr = np.arange(self.local_rows, dtype=np.int64)
+        if self.part_count <= 1:
+            return lr
+        t = lr // self.row_tile
+        return (t * self.part_count + self.part_index) * self.row_tile + lr % self.row_tile
+
+
+class Image:
+    """What RayTracePipeline::image / DiffusePipeline::image hand to the presenter."""
+
+    def __init__(self, ctx: HrtContext, image_id: int):
+        self.ctx, self.image_id = ctx, image_id
+
+    def read(self, fmt: int = _lib.FMT_RGBA8) -> np.ndarray:
+        return self.ctx.read(self.image_id, fmt)
+
+
+# ---- pipelines ---------------------------------------------------------------------------------
+
+class RayTracePipeline:
+    """src/raytrace_pipeline.rs:31-266 on the HIP context."""
+
+    def __init__(self, ctx: HrtContext, image_size, settings: RayTracerSettings):
+        self.ctx = ctx
+        self.image_size = (int(image_size[0]), int(image_size[1]))
+        rays, num_rays, jitter = create_rays(self.image_size, settings.camera_focal_length, settings.viewport_height,
+                                             settings.up)
+        spheres = sphere_records(settings.sphere_data)
+        tris, meshes = transform_meshes(settings.mesh_data if settings.mesh_data else [get_null_mesh()])
+        n_meshes = len(settings.mesh_data)
+        self.ray_count = num_rays
+        self.sphere_count = len(settings.sphere_data)
+        self.mesh_count = n_meshes
+        self.num_samples = max(int(settings.num_samples), 1)       # :88
+        self.max_bounces = max(int(settings.max_bounces), 0)       # :89
+        self.use_environment_lighting = bool(settings.use_environment_lighting)
+        self.sample_jitter = float(np.float32(settings.sample_jitter if settings.sample_jitter is not None else jitter))
+        self.tris, self.meshes, self.spheres = tris, meshes[:n_meshes], spheres
+        ctx.set_scene(rays[:num_rays], spheres, tris, meshes[:n_meshes])
+
+    def image(self) -> Image:
+        return Image(self.ctx, _lib.IMG_TRACE)
+
+    def push_constants(self, camera: Camera, rng_offset: int, init: bool) -> _lib.PushConstants:
+        """The 124-byte block of dispatch(), src/raytrace_pipeline.rs:243-257."""
+        pc = _lib.PushConstants()
+        pos = np.asarray(camera.position, np.float32)
+        pc.cam_pos[:] = [float(pos[0]), float(pos[1]), float(pos[2]), 1.0]
+        pc.cam_alignment_mat[:] = [float(v) for v in view_matrix(camera.direction, camera.up)]
+        pc.num_rays = self.ray_count
+        pc.num_spheres = self.sphere_count
+        pc.num_meshes = self.mesh_count
+        pc.num_samples = self.num_samples
+        pc.jitter_size = self.sample_jitter
+        pc.max_bounces = self.max_bounces
+        pc.use_environment_light = int(self.use_environment_lighting)
+        pc.rng_offset = int(rng_offset) & 0xFFFFFFFF
+        pc.init = int(bool(init))
+        pc.width, pc.height = self.image_size
+        return pc
+
+    def compute(self, camera: Camera, rng_offset: int) -> None:
+        self.ctx.trace(self.push_constants(camera, rng_offset, False))
+
+    def init(self) -> None:
+        self.ctx.trace(self.push_constants(Camera(), 0, True))
+
+
+class DiffusePipeline:
+    """src/diffuse.rs:22-136: the progressive accumulator (image_combiner.glsl)."""
+
+    def __init__(self, ctx: HrtContext, image_size):
+        self.ctx = ctx
+        self.image_size = (int(image_size[0]), int(image_size[1]))
+
+    def image(self) -> Image:
+        return Image(self.ctx, _lib.IMG_ACCUM)
+
+    def next_frame(self, frame_num: int, next_image: Image) -> None:
+        if next_image.ctx is not self.ctx or next_image.image_id != _lib.IMG_TRACE:
+            raise ValueError("next_image must be the trace image of the same context")
+        self.ctx.accumulate(frame_num)

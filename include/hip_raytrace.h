@@ -1,0 +1,195 @@
+/*
+ * hip_raytrace.h -- C ABI of libhip_raytrace.so, the MI355X (gfx950) drop-in for the compute side
+ * of hindlet/EPQ_Raytracer: the path-trace dispatch (assets/raytracing.glsl) and the progressive
+ * frame accumulator (assets/image_combiner.glsl).
+ *
+ * What each entry point replaces (reference paths relative to the reference repo root):
+ *   hrt_create       RayTracePipeline::new      src/raytrace_pipeline.rs:51-97   (pipeline + R8G8B8A8 image :67-73)
+ *                    DiffusePipeline::new       src/diffuse.rs:35-66             (accumulated image :50-56)
+ *   hrt_set_scene    create_ray_subbuffer / create_sphere_subbuffer / create_mesh_subbuffer uploads
+ *                                               src/raytrace_pipeline.rs:75-77, :302, :337, :349, :359, :371-372
+ *   hrt_trace        RayTracePipeline::compute  src/raytrace_pipeline.rs:162-187 (pc->init == 0)
+ *                    RayTracePipeline::init     src/raytrace_pipeline.rs:190-213 (pc->init != 0)
+ *                    -> dispatch + push constants  src/raytrace_pipeline.rs:216-266
+ *   hrt_accumulate   DiffusePipeline::next_frame src/diffuse.rs:73-101 (-> dispatch :103-136)
+ *   hrt_read_image   RayTracePipeline::image / DiffusePipeline::image  src/raytrace_pipeline.rs:156, src/diffuse.rs:69
+ *   hrt_synchronize  then_signal_fence_and_flush().unwrap() + fence wait  src/raytrace_pipeline.rs:179-183
+ *   hrt_last_error   the .unwrap() panics (every Vulkan call in src/raytrace_pipeline.rs / src/diffuse.rs)
+ *
+ * Records are byte-identical to the GLSL std430 structs (assets/raytracing.glsl:51-111) and the
+ * 124-byte push-constant block (assets/raytracing.glsl:135-153, src/raytrace_pipeline.rs:125-139),
+ * so a Rust caller can pass its raytrace_shader::* slices verbatim.
+ *
+ * Conventions: every function returns hrt_status (0 = OK).  No exceptions cross the ABI.  Host
+ * arrays are borrowed for the duration of the call only.  A context is NOT thread-safe: use it from
+ * one host thread.  All work on a context is ordered on the context's own HIP stream
+ * (== the reference's GpuFuture chaining); hrt_trace / hrt_accumulate return without waiting.
+ */
+#ifndef HIP_RAYTRACE_H
+#define HIP_RAYTRACE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HRT_ABI_VERSION 1u
+
+typedef enum hrt_status {
+  HRT_OK = 0,
+  HRT_ERR_INVALID_ARGUMENT = 1, /* bad pointer / size / count / push-constant field */
+  HRT_ERR_NO_DEVICE = 2,        /* no HIP device, or the requested ordinal does not exist */
+  HRT_ERR_OUT_OF_MEMORY = 3,
+  HRT_ERR_NO_SCENE = 4,         /* hrt_trace before hrt_set_scene */
+  HRT_ERR_HIP = 5,              /* a HIP runtime call failed; hrt_last_error has the text */
+  HRT_ERR_IO = 6                /* file not found / unparsable (host helpers) */
+} hrt_status;
+
+/* ---- std430 records (assets/raytracing.glsl:51-111) ---------------------------------------- */
+
+/* RayTracingMaterial, raytracing.glsl:51-55.  settings = (specular probability, metallic, fuzz,
+ * invisible flag == 1.0).  Built by src/materials.rs:13-94. */
+typedef struct hrt_material {
+  float colour[4];
+  float emission[4]; /* rgb, strength */
+  float settings[4];
+} hrt_material;
+
+/* Ray, raytracing.glsl:66-68: camera-space sample centre around (1,0,0) (w unused). */
+typedef struct hrt_ray {
+  float sample_centre[4];
+} hrt_ray;
+
+/* Sphere, raytracing.glsl:71-75 */
+typedef struct hrt_sphere {
+  float centre[3];
+  float radius;
+  hrt_material material;
+} hrt_sphere;
+
+/* Triangle, raytracing.glsl:79-84 (w components unused) */
+typedef struct hrt_triangle {
+  float a[4];
+  float edge_one[4]; /* b - a */
+  float edge_two[4]; /* c - a */
+  float normal[4];   /* edge_one x edge_two, NOT normalised */
+} hrt_triangle;
+
+/* Mesh, raytracing.glsl:87-93: triangles[first_index .. first_index+len) */
+typedef struct hrt_mesh {
+  float min_point[3];
+  uint32_t first_index;
+  float max_point[3];
+  uint32_t len;
+  hrt_material material;
+} hrt_mesh;
+
+/* PushConstants, raytracing.glsl:135-153 (std430, 124 bytes) */
+typedef struct hrt_push_constants {
+  float cam_pos[4];
+  float cam_alignment_mat[16]; /* column-major mat4; mat3(M) is used */
+  int32_t num_rays;
+  int32_t num_spheres;
+  int32_t num_meshes;
+  int32_t num_samples;
+  float jitter_size;
+  int32_t max_bounces;
+  uint32_t use_environment_light; /* GLSL bool */
+  uint32_t rng_offset;
+  uint32_t init; /* GLSL bool: 1 -> clear the trace image to (0,0,0,1) */
+  uint32_t width;
+  uint32_t height;
+} hrt_push_constants;
+
+/* ---- context ------------------------------------------------------------------------------ */
+
+typedef enum hrt_mode {
+  HRT_MODE_RGBA8 = 0,  /* reference-faithful: trace + accumulator images are R8G8B8A8_UNORM */
+  HRT_MODE_RGBA32F = 1 /* fp32 images, same arithmetic without the per-frame 8-bit requantization */
+} hrt_mode;
+
+typedef enum hrt_image_id { HRT_IMG_TRACE = 0, HRT_IMG_ACCUM = 1 } hrt_image_id;
+typedef enum hrt_format { HRT_FMT_RGBA8 = 0, HRT_FMT_RGBA32F = 1 } hrt_format;
+
+typedef struct hrt_create_info {
+  uint32_t width;      /* full image size (image_size[0]) */
+  uint32_t height;     /* image_size[1] */
+  int32_t device;      /* HIP device ordinal; -1 = the calling thread's current device */
+  uint32_t mode;       /* hrt_mode */
+  /* Image-space partition (multi-GPU row tiles).  Rows are grouped into tiles of
+   * row_tile rows; this context renders tiles t with t % part_count == part_index and stores them
+   * compacted (local row r <-> global row ((r / row_tile) * part_count + part_index) * row_tile
+   * + r % row_tile).  part_count == 0 or 1 means the whole image. */
+  uint32_t row_tile;
+  uint32_t part_index;
+  uint32_t part_count;
+} hrt_create_info;
+
+typedef struct hrt_layout {
+  uint32_t width, height;   /* full image */
+  uint32_t local_rows;      /* rows stored by this context (padded: equal on every part) */
+  uint32_t row_tile, part_index, part_count;
+  uint32_t mode;
+} hrt_layout;
+
+typedef struct hrt_stats {
+  uint64_t segments;      /* world_hit calls (raytracing.glsl:317) over all traces since reset */
+  uint64_t tri_tests;     /* ray-triangle tests (Sum over AABB-passing meshes of len) since reset */
+  uint64_t traces;        /* non-init trace dispatches since reset */
+  uint64_t accumulates;   /* combiner dispatches since reset */
+  float last_trace_ms;    /* device time of the last trace dispatch (HIP events) */
+  float total_trace_ms;   /* device time of all trace dispatches since reset */
+} hrt_stats;
+
+typedef struct hrt_context hrt_context;
+
+/* Option keys for hrt_set_option. */
+typedef enum hrt_option {
+  /* kernel variant: 0 = tuned (default), 1 = literal per-sample loop (same results, A/B and parity) */
+  HRT_OPT_KERNEL_VARIANT = 1,
+  /* 1 = count segments / triangle tests on the device (default 1; 0 removes the counters' cost) */
+  HRT_OPT_COUNTERS = 2
+} hrt_option;
+
+uint32_t hrt_abi_version(void);
+
+hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_ctx);
+void hrt_destroy(hrt_context* ctx);
+
+/* Upload the scene.  rays: n_rays == width*height records indexed by global pixel id x + y*W.
+ * spheres/tris/meshes may be NULL when their count is 0 (the reference's "null object" records are
+ * not needed).  Every mesh range must lie inside [0, n_tri).  Copies before returning. */
+hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint32_t n_rays, const hrt_sphere* spheres,
+                         uint32_t n_spheres, const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes,
+                         uint32_t n_meshes);
+
+/* One dispatch of raytracing.glsl (or its init clear when pc->init != 0).  pc->width/height must
+ * equal the context's; pc->num_spheres/num_meshes must not exceed the uploaded counts. */
+hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc);
+
+/* One dispatch of image_combiner.glsl with next_image = this context's trace image. */
+hrt_status hrt_accumulate(hrt_context* ctx, uint32_t frame);
+
+/* Copy this context's local rows of an image (row-major, local_rows x width x 4 channels) into dst,
+ * which may be host or device memory.  Blocking.  bytes must be >= the image size in fmt. */
+hrt_status hrt_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes);
+
+hrt_status hrt_get_layout(const hrt_context* ctx, hrt_layout* out);
+hrt_status hrt_synchronize(hrt_context* ctx);
+hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out); /* synchronizes */
+hrt_status hrt_reset_stats(hrt_context* ctx);
+hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
+
+/* HIP stream the context's work is ordered on (hipStream_t), for callers that interoperate. */
+void* hrt_stream(hrt_context* ctx);
+
+/* Text of the last error on ctx (or of the last hrt_create failure when ctx is NULL). */
+const char* hrt_last_error(const hrt_context* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HIP_RAYTRACE_H */
