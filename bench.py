@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s of the MI355X path tracer on the headline workload of BASELINE.json
+(island.obj, 1920x1080, 64 spp, 8 bounces) -- one "step" = one progressive frame: one trace dispatch
+(64 samples per pixel, rng_offset = frame index) + one accumulate dispatch (+ the row-tile gather of
+the framebuffer when N > 1).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+A "ray" is one segment = one world_hit call (assets/raytracing.glsl:317), counted exactly on the
+device.  value = segments of all ranks / max-over-ranks wall time of the K timed steps.
+Prints ONE JSON line on rank 0 (fields: DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
+FLOP_PER_TEST = 38         # algorithmic fp32 FLOP per ray-triangle test (raytracing.glsl:213-241)
+BYTES_PER_PIXEL_FRAME = 32  # 16 B ray centre + 4 B trace store + 12 B combiner (r, r, w)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="island")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=64, help="samples per pixel per frame (num_samples)")
+    ap.add_argument("--bounces", type=int, default=8, help="max_bounces")
+    ap.add_argument("--variant", type=int, default=0, help="0 tuned, 1 literal")
+    ap.add_argument("--row-tile", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length (0 = skip)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="rocprofv3 PMC summary giving HBM bytes per trace launch for this workload")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    dist_on = world > 1
+    if dist_on:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import epq_raytracer_amd as E
+    from epq_raytracer_amd import _lib, rowtiles
+
+    W, H = args.width, args.height
+    camera, settings = E.PRESETS[args.scene]()
+    settings.num_samples, settings.max_bounces = args.spp, args.bounces
+    partition = (args.row_tile, rank, world) if dist_on else None
+    ctx = E.HrtContext((W, H), device=local_rank, mode=_lib.MODE_RGBA8, partition=partition)
+    raytrace = E.RayTracePipeline(ctx, (W, H), settings)
+    diffuse = E.DiffusePipeline(ctx, (W, H))
+    ctx.set_option(_lib.OPT_KERNEL_VARIANT, args.variant)
+    raytrace.init()
+    diffuse.next_frame(0, raytrace.image())
+    frame = 1
+
+    local = torch.empty((ctx.local_rows, W, 4), dtype=torch.uint8, device=f"cuda:{local_rank}") if dist_on else None
+
+    def step():
+        nonlocal frame
+        raytrace.compute(camera, frame)
+        diffuse.next_frame(frame, raytrace.image())
+        frame += 1
+        if dist_on:
+            ctx.read_into(_lib.IMG_ACCUM, _lib.FMT_RGBA8, local.data_ptr(), local.numel())
+            rowtiles.gather_frame(local, H, args.row_tile)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    ctx.reset_stats()
+
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    st = ctx.stats()
+    segs, tests = st.segments, st.tri_tests
+    kern_ms = st.total_trace_ms / max(st.traces, 1)
+    if dist_on:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+        c = torch.tensor([segs, tests], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        segs_all, tests_all = int(c[0]), int(c[1])
+    else:
+        kern_ms_max, segs_all, tests_all = kern_ms, segs, tests
+
+    if rank == 0:
+        ms_per_step = elapsed * 1e3 / args.steps
+        value = segs_all / elapsed / 1e6
+        # roofline of the dominant kernel (trace), rank 0's launches: algorithmic FLOP / launch time
+        tests_per_launch = tests / max(st.traces, 1)
+        achieved_tf = FLOP_PER_TEST * tests_per_launch / (kern_ms * 1e-3) / 1e12
+        pix_local = ctx.local_rows * W
+        algo_bytes = BYTES_PER_PIXEL_FRAME * pix_local + (len(raytrace.tris) * 64 + len(raytrace.meshes) * 80)
+        traffic = None
+        pmc_note = None
+        if os.path.exists(args.pmc_json):
+            with open(args.pmc_json) as f:
+                pmc = json.load(f)
+            wl = pmc.get("workload", {})
+            if (wl.get("scene"), wl.get("width"), wl.get("height"), wl.get("spp"), wl.get("bounces")) == \
+                    (args.scene, W, H, args.spp, args.bounces) and world == 1:
+                traffic = pmc.get("hbm_bytes_per_trace_launch")
+                pmc_note = os.path.relpath(args.pmc_json, ROOT)
+        line = {
+            "metric": "Mrays/s (island.obj 1080p 64spp 8-bounce path-trace segments per second)",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference scene preset (island.obj geometry + src/main.rs materials/camera), "
+                    "deterministic RNG seeds rng_offset = frame index",
+            "config": {"workload": f"{args.scene}.obj {W}x{H} {args.spp}spp {args.bounces}-bounce, 1 frame/step "
+                                   f"(trace + accumulate{' + row-tile gather' if dist_on else ''})",
+                       "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
+                       "parallelism": f"row-tiles{world}x{args.row_tile}" if dist_on else "single-gpu",
+                       "kernel_variant": "tuned" if args.variant == 0 else "literal"},
+            "segments_per_step": segs_all // args.steps,
+            "tri_tests_per_step": tests_all // args.steps,
+            "paths_per_s": W * H * args.spp / (elapsed / args.steps),
+            "roofline": {"bound": "valu-fp32", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
+                         "traffic": traffic,
+                         "kernel": "hrt::trace_tuned" if args.variant == 0 else "hrt::trace_literal",
+                         "kernel_ms": round(kern_ms, 3), "flop_per_test": FLOP_PER_TEST,
+                         "tests_per_launch": int(tests_per_launch), "pmc_source": pmc_note},
+            "hbm_roofline": {"achieved": round(algo_bytes / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(algo_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
+                             "algorithmic_bytes_per_launch": algo_bytes, "traffic": traffic},
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            line["cpu_baseline"], line["parity_sample"] = cpu_baseline(args, ctx, raytrace, camera)
+        print(json.dumps(line), flush=True)
+
+    ctx.close()
+    if dist_on:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, ctx, raytrace, camera):
+    """The oracle (oracle/rt_oracle.c, OpenMP) on a bounded sample of the same workload: whole rows
+    spread evenly over the frame, frame rng_offset = 1.  Also checks those rows of the GPU frame
+    byte for byte against it (the same rows, traced again on the GPU with rng_offset = 1)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from epq_raytracer_amd import _lib
+
+    W, H = args.width, args.height
+    pc = raytrace.push_constants(camera, 1, False)
+    rays = raytrace.rays
+    threads = pyoracle.num_threads()
+    # calibrate on one row, then pick a row count for ~cpu_seconds
+    t = time.perf_counter()
+    pyoracle.trace(pc, rays, raytrace.spheres, raytrace.tris, raytrace.meshes, rows=(H // 2, H // 2 + 1))
+    per_row = max(time.perf_counter() - t, 1e-4)
+    nrows = int(min(H, max(2, args.cpu_seconds / per_row)))
+    rows = np.unique(np.linspace(0, H - 1, nrows).astype(int))
+    segs = 0
+    cpu_img = np.zeros((H, W, 4), np.uint8)
+    t = time.perf_counter()
+    for y in rows:
+        img, _, s, _ = pyoracle.trace(pc, rays, raytrace.spheres, raytrace.tris, raytrace.meshes, rows=(int(y), int(y) + 1))
+        cpu_img[y] = img[y]
+        segs += s
+    dt = time.perf_counter() - t
+    # GPU frame with the same rng_offset, same rows
+    ctx.trace(pc)
+    gpu = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+    same = bool(np.array_equal(gpu[rows], cpu_img[rows]))
+    base = {"value": round(segs / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{len(rows)} of {H} rows (evenly spaced) of the same frame (rng_offset=1), {segs} segments, "
+                      f"{dt:.1f} s on {threads} OpenMP threads (oracle/rt_oracle.c -O2 -ffp-contract=off)"}
+    parity = {"rows_checked": int(len(rows)), "bit_exact": same}
+    return base, parity
+
+
+if __name__ == "__main__":
+    main()

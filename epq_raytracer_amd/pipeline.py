@@ -199,7 +199,7 @@ class RayTracePipeline:
         self.max_bounces = max(int(settings.max_bounces), 0)       # :89
         self.use_environment_lighting = bool(settings.use_environment_lighting)
         self.sample_jitter = float(np.float32(settings.sample_jitter if settings.sample_jitter is not None else jitter))
-        self.tris, self.meshes, self.spheres = tris, meshes[:n_meshes], spheres
+        self.rays, self.tris, self.meshes, self.spheres = rays[:num_rays], tris, meshes[:n_meshes], spheres
         ctx.set_scene(rays[:num_rays], spheres, tris, meshes[:n_meshes])
 
     def image(self) -> Image:
