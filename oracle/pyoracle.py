@@ -39,6 +39,8 @@ def load(prefer_fma: bool | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    if prefer_fma is None and os.environ.get("ORC_VARIANT") in ("fma", "generic"):
+        prefer_fma = os.environ["ORC_VARIANT"] == "fma"
     fma = _cpu_has_fma() if prefer_fma is None else prefer_fma
     path = os.path.join(BUILD, "liborc_fma.so" if fma else "liborc.so")
     if not os.path.exists(path):
@@ -135,13 +137,15 @@ def unorm8(x: float) -> int:
 
 
 def intersecting_aabb(mn, mx, o, d) -> bool:
-    return bool(load().orc_intersecting_aabb(_p(_f32(mn, 3)), _p(_f32(mx, 3)), _p(_f32(o, 3)), _p(_f32(d, 3))))
+    keep = [_f32(v, 3) for v in (mn, mx, o, d)]  # arrays must outlive the call
+    return bool(load().orc_intersecting_aabb(*[_p(a) for a in keep]))
 
 
 def intersecting_tri(tri_record: np.ndarray, o, d) -> np.ndarray:
     out = np.zeros(4, np.float32)
-    t = np.ascontiguousarray(tri_record)
-    load().orc_intersecting_tri(_p(t.view(np.uint8)), _p(_f32(o, 3)), _p(_f32(d, 3)), _p(out))
+    t = np.ascontiguousarray(tri_record).view(np.uint8)
+    oo, dd = _f32(o, 3), _f32(d, 3)
+    load().orc_intersecting_tri(_p(t), _p(oo), _p(dd), _p(out))
     return out
 
 
@@ -149,14 +153,16 @@ def intersecting_tri(tri_record: np.ndarray, o, d) -> np.ndarray:
 
 def view_matrix(direction, up) -> np.ndarray:
     out = np.zeros(16, np.float32)
-    load().orc_view_matrix(_p(_f32(direction, 3)), _p(_f32(up, 3)), _p(out))
+    d, u = _f32(direction, 3), _f32(up, 3)
+    load().orc_view_matrix(_p(d), _p(u), _p(out))
     return out
 
 
 def create_rays(w: int, h: int, focal: float, vh: float, up):
     out = np.zeros((max(w * h, 1), 4), np.float32)
     jit = c_float()
-    n = load().orc_create_rays(w, h, focal, vh, _p(_f32(up, 3)), _p(out), ctypes.byref(jit))
+    u = _f32(up, 3)
+    n = load().orc_create_rays(w, h, focal, vh, _p(u), _p(out), ctypes.byref(jit))
     return out[:n], n, jit.value
 
 
@@ -174,7 +180,8 @@ def transform_meshes(meshes, tri_dtype, mesh_dtype, material_dtype):
         mn = np.zeros(3, np.float32)
         mx = np.zeros(3, np.float32)
         sub = np.zeros(max(n, 1), dtype=tri_dtype)
-        lib.orc_transform_mesh(_p(pos), _p(idx), len(idx), _p(sub.view(np.uint8)), _p(mn), _p(mx))
+        sub_b = sub.view(np.uint8)
+        lib.orc_transform_mesh(_p(pos), _p(idx), len(idx), _p(sub_b), _p(mn), _p(mx))
         tris[first:first + n] = sub[:n]
         recs[k]["min_point"] = mn
         recs[k]["max_point"] = mx
@@ -197,29 +204,31 @@ def trace(pc, rays, spheres, tris, meshes, rows=None, nthreads: int = 0, want_f3
     img8 = np.zeros((H, W, 4), np.uint8)
     img32 = np.zeros((H, W, 4), np.float32) if want_f32 else None
     seg, tt = c_uint64(), c_uint64()
-    rays = np.ascontiguousarray(rays)
-    lib.orc_trace_rows(ctypes.byref(pc), _p(rays.view(np.uint8)), _p(_bytes(spheres)), _p(_bytes(tris)),
-                       _p(_bytes(meshes)), y0, y1, _p(img8), _p(img32), ctypes.byref(seg), ctypes.byref(tt),
-                       int(nthreads))
+    keep = [np.ascontiguousarray(rays).view(np.uint8), _bytes(spheres), _bytes(tris), _bytes(meshes)]
+    lib.orc_trace_rows(ctypes.byref(pc), *[_p(a) for a in keep], y0, y1, _p(img8), _p(img32), ctypes.byref(seg),
+                       ctypes.byref(tt), int(nthreads))
     return img8, img32, seg.value, tt.value
 
 
 def trace_pixel(pc, rays, spheres, tris, meshes, x: int, y: int):
     out = np.zeros(3, np.float32)
     seg, tt = c_uint64(), c_uint64()
-    load().orc_trace_pixel(ctypes.byref(pc), _p(np.ascontiguousarray(rays).view(np.uint8)), _p(_bytes(spheres)),
-                           _p(_bytes(tris)), _p(_bytes(meshes)), x, y, _p(out), ctypes.byref(seg), ctypes.byref(tt))
+    keep = [np.ascontiguousarray(rays).view(np.uint8), _bytes(spheres), _bytes(tris), _bytes(meshes)]
+    load().orc_trace_pixel(ctypes.byref(pc), *[_p(a) for a in keep], x, y, _p(out), ctypes.byref(seg),
+                           ctypes.byref(tt))
     return out, seg.value, tt.value
 
 
 def accumulate_rgba8(frame: int, current: np.ndarray, new_image: np.ndarray) -> None:
     assert current.dtype == np.uint8 and new_image.dtype == np.uint8 and current.shape == new_image.shape
-    load().orc_accumulate_rgba8(frame, _p(current), _p(np.ascontiguousarray(new_image)), current.size // 4)
+    nw = np.ascontiguousarray(new_image)
+    load().orc_accumulate_rgba8(frame, _p(current), _p(nw), current.size // 4)
 
 
 def accumulate_rgba32f(frame: int, current: np.ndarray, new_image: np.ndarray) -> None:
     assert current.dtype == np.float32 and current.shape == new_image.shape
-    load().orc_accumulate_rgba32f(frame, _p(current), _p(np.ascontiguousarray(new_image)), current.size // 4)
+    nw = np.ascontiguousarray(new_image)
+    load().orc_accumulate_rgba32f(frame, _p(current), _p(nw), current.size // 4)
 
 
 def num_threads() -> int:

@@ -1,0 +1,92 @@
+"""The C ABI (CPU): libhip_raytrace.so loads, exports exactly what include/*.h declares, the record
+layouts are the std430 ones, and calls fail loudly (status + message) instead of falling back."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from epq_raytracer_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    names = set()
+    for h in ("hip_raytrace.h", "hrt_host.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(hrt_[a-z0-9_]+)\s*\(", src))
+    return names
+
+
+def test_every_declared_symbol_is_exported():
+    declared = _declared_functions()
+    assert declared == set(_lib.EXPORTED_SYMBOLS)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = {line.split()[-1] for line in out.stdout.splitlines() if " T " in line}
+    missing = declared - exported
+    assert not missing, missing
+
+
+def test_library_loads_and_reports_abi():
+    lib = _lib.load()
+    assert lib.hrt_abi_version() == 1
+
+
+def test_code_object_targets_gfx950():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob  # the fat binary carries a gfx950 code object
+    assert b"trace_tuned" in blob and b"trace_literal" in blob
+
+
+def test_record_layouts_match_std430():
+    assert _lib.MATERIAL_DTYPE.itemsize == 48
+    assert _lib.SPHERE_DTYPE.fields["material"][1] == 16
+    assert _lib.MESH_DTYPE.fields["first_index"][1] == 12
+    assert _lib.MESH_DTYPE.fields["len"][1] == 28
+    assert _lib.MESH_DTYPE.fields["material"][1] == 32
+    assert ctypes.sizeof(_lib.PushConstants) == 124
+    assert _lib.PushConstants.num_rays.offset == 80
+    assert _lib.PushConstants.jitter_size.offset == 96
+    assert _lib.PushConstants.use_environment_light.offset == 104
+    assert _lib.PushConstants.height.offset == 120
+
+
+def test_create_fails_loudly():
+    lib = _lib.load()
+    info = _lib.CreateInfo(0, 0, -1, 0, 0, 0, 1)
+    h = ctypes.c_void_p()
+    st = lib.hrt_create(ctypes.byref(info), ctypes.byref(h))
+    assert st == 1 and not h.value  # zero size -> HRT_ERR_INVALID_ARGUMENT, no context
+    assert b"zero image size" in lib.hrt_last_error(None)
+    info = _lib.CreateInfo(8, 8, -1, 7, 0, 0, 1)
+    assert lib.hrt_create(ctypes.byref(info), ctypes.byref(h)) == 1  # unknown mode
+    info = _lib.CreateInfo(8, 8, -1, 0, 0, 0, 2)
+    assert lib.hrt_create(ctypes.byref(info), ctypes.byref(h)) == 1  # partition without row_tile
+
+
+def test_no_cpu_fallback_without_device():
+    lib = _lib.load()
+    info = _lib.CreateInfo(8, 8, -1, 0, 0, 0, 1)
+    h = ctypes.c_void_p()
+    st = lib.hrt_create(ctypes.byref(info), ctypes.byref(h))
+    if st == 0:
+        lib.hrt_destroy(h)
+        pytest.skip("a GPU is visible here")
+    assert st == 2, _lib.STATUS_NAMES.get(st)  # HRT_ERR_NO_DEVICE: there is no CPU path
+    with pytest.raises(_lib.HrtError):
+        import epq_raytracer_amd as E
+        E.HrtContext((8, 8))
+
+
+def test_null_handles_are_rejected():
+    lib = _lib.load()
+    pc = _lib.PushConstants()
+    assert lib.hrt_trace(None, ctypes.byref(pc)) == 1
+    assert lib.hrt_accumulate(None, 1) == 1
+    assert lib.hrt_synchronize(None) == 1
+    buf = np.zeros(4, np.uint8)
+    assert lib.hrt_read_image(None, 0, 0, _lib.ptr(buf), 4) == 1

@@ -1,0 +1,60 @@
+"""Golden fixtures (CPU): the oracle reproduces tests/golden (made by tests/golden/make_golden.py),
+and its FMA and generic builds agree bit for bit (explicit fmaf either way: numerics spec S2)."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import pyoracle
+from helpers import SceneCase
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+META = json.load(open(os.path.join(GOLD, "golden.json")))
+
+
+@pytest.fixture(scope="module")
+def arrays():
+    with np.load(os.path.join(GOLD, "golden.npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("name", sorted(META["frames"]))
+def test_oracle_reproduces_golden_frame(name, arrays):
+    m = META["frames"][name]
+    case = SceneCase(m["scene"], tuple(m["size"]), m["spp"], m["bounces"], rng_offset=m["rng_offset"])
+    img, f32, seg, tt = case.oracle(want_f32=True)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == m["sha256_rgba8"]
+    np.testing.assert_array_equal(img, arrays[name])
+    np.testing.assert_array_equal(f32.view(np.uint32), arrays[name + "_f32"].view(np.uint32))
+    assert (seg, tt) == (m["segments"], m["tri_tests"])
+
+
+def test_golden_pixels():
+    for p in META["pixels"]:
+        m = META["frames"][p["frame"]]
+        c = SceneCase(m["scene"], tuple(m["size"]), m["spp"], m["bounces"], rng_offset=m["rng_offset"])
+        rgb, seg, tt = pyoracle.trace_pixel(c.push(), c.rays, c.spheres, c.tris, c.meshes, p["x"], p["y"])
+        assert [int(v) for v in rgb.view(np.uint32)] == p["rgb_bits"]
+        assert (seg, tt) == (p["segments"], p["tri_tests"])
+
+
+def test_golden_rng():
+    for seed, seq in META["rng"].items():
+        assert pyoracle.hash_sequence(int(seed), 8) == seq
+
+
+def test_fma_and_generic_oracle_builds_agree():
+    code = ("import sys, hashlib; sys.path[:0] = [%r, %r]; from helpers import SceneCase; "
+            "img = SceneCase('island', (48, 27), 2, 8).oracle()[0]; print(hashlib.sha256(img.tobytes()).hexdigest())"
+            % (HERE, os.path.join(os.path.dirname(HERE), "oracle")))
+    outs = []
+    for variant in ("fma", "generic"):
+        env = dict(os.environ, ORC_VARIANT=variant, OMP_NUM_THREADS="2")
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, check=True)
+        outs.append(r.stdout.strip())
+    assert outs[0] == outs[1] and len(outs[0]) == 64

@@ -1,0 +1,267 @@
+"""GPU parity (MI355X): the HIP path through the C ABI against the CPU oracle, byte for byte, with
+the device's segment / triangle-test counters equal to the oracle's exact counts.
+
+Bar: rgba8 frames identical (integer output of a pinned fp32 computation, DESIGN.md numerics spec);
+rgba32f frames bitwise identical.  This is stricter than north_star's per-channel |delta| <= 1e-4.
+Full-size (1920x1080 64 spp) frames are checked on oracle-computed rows spread over the frame plus
+size-independent properties (determinism, variant agreement, partition reassembly)."""
+import numpy as np
+import pytest
+
+import pyoracle
+from helpers import E, SceneCase, _lib, mismatch_report
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = [0, 1]  # tuned, literal
+
+CONFIGS = [
+    # (scene, size, spp, bounces, rng_offset)
+    ("cube", (256, 256), 1, 1, 1),      # configs[0] shape (C1)
+    ("box", (512, 512), 16, 4, 1),      # configs[1]: first-kernel correctness gate (C2)
+    ("box", (128, 128), 4, 50, 7),      # the reference preset's 50 bounces
+    ("island", (192, 108), 8, 8, 1),    # headline scene, small
+    ("island", (64, 64), 4, 12, 5),     # C5's bounce count
+    ("cave", (128, 72), 4, 8, 1),       # configs[2] scene, small
+    ("spheres", (96, 72), 4, 8, 2),     # spheres + invisible light sphere
+    ("box", (37, 23), 3, 5, 1),         # ragged: not a multiple of the 16x16 tile
+    ("island", (1, 1), 2, 8, 1),
+    ("box", (300, 1), 2, 4, 1),
+    ("box", (1, 130), 2, 4, 1),
+]
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("scene,size,spp,bounces,off", CONFIGS)
+def test_frame_bit_exact(scene, size, spp, bounces, off, variant):
+    case = SceneCase(scene, size, spp, bounces, rng_offset=off)
+    ref, _, seg, tt = case.oracle()
+    img, gseg, gtt = case.gpu(variant=variant)
+    assert np.array_equal(img, ref), mismatch_report(img, ref)
+    assert (gseg, gtt) == (seg, tt)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_rgba32f_mode_bitwise(variant):
+    case = SceneCase("island", (96, 54), 4, 8)
+    _, ref32, seg, _ = case.oracle(want_f32=True)
+    img32, gseg, _ = case.gpu(mode=_lib.MODE_RGBA32F, variant=variant, fmt=_lib.FMT_RGBA32F)
+    np.testing.assert_array_equal(img32.view(np.uint32), ref32.view(np.uint32))
+    assert gseg == seg
+    # fp32 context read back as rgba8 applies the same UNORM store rule
+    img8, _, _ = case.gpu(mode=_lib.MODE_RGBA32F, variant=variant, fmt=_lib.FMT_RGBA8)
+    ref8, _, _, _ = case.oracle()
+    assert np.array_equal(img8, ref8)
+
+
+def test_golden_frames_on_gpu():
+    import json
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    meta = json.load(open(os.path.join(here, "golden", "golden.json")))
+    with np.load(os.path.join(here, "golden", "golden.npz"), allow_pickle=False) as z:
+        for name, m in meta["frames"].items():
+            case = SceneCase(m["scene"], tuple(m["size"]), m["spp"], m["bounces"], rng_offset=m["rng_offset"])
+            img, seg, tt = case.gpu()
+            assert np.array_equal(img, z[name]), name
+            assert (seg, tt) == (m["segments"], m["tri_tests"]), name
+
+
+@pytest.mark.parametrize("mode", [_lib.MODE_RGBA8, _lib.MODE_RGBA32F])
+def test_progressive_accumulation_matches_oracle(mode):
+    """RayTracingApp sequencing (src/raytracing_app.rs:74-227): open clears with frame 0, frame k
+    traces with rng_offset = k and folds into the accumulator with weight k."""
+    cam, st = E.load_box_scene()
+    st.num_samples, st.max_bounces = 2, 4
+    size = (64, 48)
+    app = E.RayTracingApp(cam, st, device=0, mode=mode)
+    app.open(size)
+    E.compute_then_render(app, 0.016)
+    E.compute_n_then_render(app, 4)
+    assert app.frame == 6
+    fmt = _lib.FMT_RGBA8 if mode == _lib.MODE_RGBA8 else _lib.FMT_RGBA32F
+    got = app.pipeline[1].image().read(fmt)
+    app.close()
+    case = SceneCase("box", size, 2, 4)
+    if mode == _lib.MODE_RGBA8:
+        acc = np.zeros((size[1], size[0], 4), np.uint8)
+        pyoracle.accumulate_rgba8(0, acc, acc.copy())
+        for k in range(1, 6):
+            pyoracle.accumulate_rgba8(k, acc, case.oracle(rng_offset=k)[0])
+        assert np.array_equal(got, acc), mismatch_report(got, acc)
+    else:
+        acc = np.zeros((size[1], size[0], 4), np.float32)
+        pyoracle.accumulate_rgba32f(0, acc, acc.copy())
+        for k in range(1, 6):
+            pyoracle.accumulate_rgba32f(k, acc, case.oracle(rng_offset=k, want_f32=True)[1])
+        np.testing.assert_array_equal(got.view(np.uint32), acc.view(np.uint32))
+
+
+@pytest.mark.parametrize("parts,tile", [(2, 16), (3, 16), (8, 4)])
+def test_row_tile_partition_reassembles_full_frame(parts, tile):
+    from epq_raytracer_amd import rowtiles
+    case = SceneCase("island", (80, 70), 2, 8)
+    ref, _, seg, tt = case.oracle()
+    stacked, segs, tests = [], 0, 0
+    for p in range(parts):
+        ctx = case.context(partition=(tile, p, parts))
+        ctx.trace(case.push())
+        ctx.accumulate(1)
+        s = ctx.stats()
+        segs, tests = segs + s.segments, tests + s.tri_tests
+        np.testing.assert_array_equal(ctx.global_rows(), rowtiles.global_rows(70, tile, parts, p))
+        stacked.append(ctx.read(_lib.IMG_TRACE))
+        ctx.close()
+    full = np.concatenate(stacked)[rowtiles.assembly_index(70, tile, parts)]
+    assert np.array_equal(full, ref), mismatch_report(full, ref)
+    assert (segs, tests) == (seg, tt)
+
+
+def test_empty_scene_env_and_black():
+    settings = E.RayTracerSettings(num_samples=3, max_bounces=4, use_environment_lighting=True)
+    cam = E.Camera([0, 0, 0], [1, 0.5, 0.2])
+    for env in (True, False):
+        settings.use_environment_lighting = env
+        case = SceneCase(settings=settings, camera=cam, size=(40, 30), num_samples=3, max_bounces=4)
+        ref, _, seg, tt = case.oracle()
+        img, gseg, gtt = case.gpu()
+        assert np.array_equal(img, ref)
+        assert gseg == seg == 40 * 30 * 3 and gtt == tt == 0
+        if not env:
+            assert not img[..., :3].any()
+
+
+@pytest.mark.parametrize("bounces", [0, 1])
+def test_low_bounce_counts(bounces):
+    for variant in VARIANTS:
+        case = SceneCase("box", (64, 64), 3, bounces)
+        ref, _, seg, tt = case.oracle()
+        img, gseg, gtt = case.gpu(variant=variant)
+        assert np.array_equal(img, ref) and (gseg, gtt) == (seg, tt)
+
+
+def test_rng_offset_wraps():
+    for off in (0, 0xFFFFFFFF, 123456789):
+        case = SceneCase("box", (48, 48), 2, 4, rng_offset=off)
+        ref = case.oracle()[0]
+        assert np.array_equal(case.gpu()[0], ref), off
+
+
+def _soup(n, seed=0x5EED, lo=-10.0, hi=10.0):
+    rng = np.random.default_rng(seed)
+    v = rng.uniform(lo, hi, size=(n * 3, 3)).astype(np.float32)
+    return E.Mesh(v, np.arange(n * 3, dtype=np.uint32))
+
+
+@pytest.mark.parametrize("n", [256, 1024])
+def test_triangle_soup(n):
+    """The roofline sweep's synthetic scene: uniform triangle soup, island camera."""
+    cam, _ = E.load_island_scene()
+    st = E.RayTracerSettings(num_samples=2, max_bounces=6, use_environment_lighting=True,
+                             mesh_data=[E.RayTracingMesh(_soup(n), E.LambertianMaterial([0.5, 0.5, 0.5]))])
+    case = SceneCase(settings=st, camera=E.Camera([0.0, 0.0, -25.0], [0.0, 0.0, 1.0]), size=(96, 96),
+                     num_samples=2, max_bounces=6)
+    ref, _, seg, tt = case.oracle()
+    for variant in VARIANTS:
+        img, gseg, gtt = case.gpu(variant=variant)
+        assert np.array_equal(img, ref), mismatch_report(img, ref)
+        assert (gseg, gtt) == (seg, tt)
+
+
+def test_degenerate_and_adversarial_geometry():
+    """Stresses the tuned kernel's exact cull: sliver and zero-area triangles, near-parallel
+    (tiny det) hits, duplicate triangles (ties: the first in buffer order wins), huge and tiny
+    coordinates, and a sphere tying with a triangle."""
+    rng = np.random.default_rng(11)
+    tris = []
+    for _ in range(200):  # slivers: c almost on the line a-b
+        a = rng.uniform(-3, 3, 3)
+        b = a + rng.uniform(-2, 2, 3)
+        c = a + (b - a) * rng.uniform(0, 1) + rng.normal(size=3) * 1e-6
+        tris += [a, b, c]
+    for _ in range(50):  # zero-area triangles
+        a = rng.uniform(-3, 3, 3)
+        tris += [a, a, a + rng.uniform(-1, 1, 3)]
+    for _ in range(100):  # near-edge-on to the camera's view (-z axis): nearly parallel to rays
+        a = rng.uniform(-3, 3, 3)
+        tris += [a, a + np.array([2.0, 0.0, 1e-5]), a + np.array([0.0, 0.0, 2.0])]
+    base = np.array([[-2.0, -2.0, 1.0], [2.0, -2.0, 1.0], [0.0, 2.0, 1.0]])
+    tris += list(base) + list(base)  # exact duplicate: tie
+    tris += [np.array([-1e6, -1e6, 50.0]), np.array([1e6, -1e6, 50.0]), np.array([0.0, 1e6, 50.0])]  # huge
+    tris += [np.array([0.0, 0.0, 2.0]), np.array([1e-30, 0.0, 2.0]), np.array([0.0, 1e-30, 2.0])]  # tiny
+    v = np.array(tris, np.float32)
+    mesh = E.Mesh(v, np.arange(len(v), dtype=np.uint32))
+    mesh_b = E.Mesh(v[::-1].copy(), np.arange(len(v), dtype=np.uint32))  # opposite winding copy
+    st = E.RayTracerSettings(num_samples=3, max_bounces=8, use_environment_lighting=True,
+                             sphere_data=[E.Sphere([0.0, 0.0, 1.0], 0.5, E.MetalMaterial([0.9, 0.9, 0.9], 1.0, 0.0))],
+                             mesh_data=[E.RayTracingMesh(mesh, E.LambertianMaterial([0.8, 0.7, 0.6])),
+                                        E.RayTracingMesh(mesh_b, E.MetalMaterial([0.6, 0.7, 0.9], 0.8, 0.1))])
+    case = SceneCase(settings=st, camera=E.Camera([0.1, 0.2, -6.0], [0.0, 0.0, 1.0]), size=(128, 128),
+                     num_samples=3, max_bounces=8)
+    ref, _, seg, tt = case.oracle()
+    for variant in VARIANTS:
+        img, gseg, gtt = case.gpu(variant=variant)
+        assert np.array_equal(img, ref), mismatch_report(img, ref)
+        assert (gseg, gtt) == (seg, tt)
+
+
+def test_errors_fail_loudly():
+    case = SceneCase("box", (32, 32), 1, 1)
+    ctx = E.HrtContext((32, 32), device=0)
+    with pytest.raises(_lib.HrtError, match="NO_SCENE"):
+        ctx.trace(case.push())
+    ctx.set_scene(case.rays, case.spheres, case.tris, case.meshes)
+    pc = case.push()
+    pc.width = 33
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        ctx.trace(pc)
+    pc = case.push()
+    pc.num_meshes = len(case.meshes) + 1
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        ctx.trace(pc)
+    bad = case.meshes.copy()
+    bad[0]["len"] = 10 ** 6
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        ctx.set_scene(case.rays, case.spheres, case.tris, bad)
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        ctx.read_into(_lib.IMG_TRACE, _lib.FMT_RGBA8, np.zeros(4, np.uint8).ctypes.data, 4)
+    ctx.close()
+
+
+# ---- full size (1920x1080, 64 spp, 8 bounces: the headline workload) ------------------------
+
+@pytest.fixture(scope="module")
+def headline():
+    case = SceneCase("island", (1920, 1080), 64, 8, rng_offset=1)
+    ctx = case.context()
+    ctx.trace(case.push(1))
+    img1 = ctx.read(_lib.IMG_TRACE)
+    st = ctx.stats()
+    ctx.trace(case.push(1))
+    img1b = ctx.read(_lib.IMG_TRACE)
+    ctx.trace(case.push(2))
+    img2 = ctx.read(_lib.IMG_TRACE)
+    ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
+    ctx.trace(case.push(1))
+    lit = ctx.read(_lib.IMG_TRACE)
+    ctx.close()
+    return case, img1, img1b, img2, lit, st
+
+
+def test_headline_rows_bit_exact(headline):
+    case, img1, _, _, _, st = headline
+    rows = [0, 137, 300, 421, 540, 611, 777, 901, 1079]
+    for y in rows:
+        ref = case.oracle(rows=(y, y + 1))[0]
+        assert np.array_equal(img1[y], ref[y]), f"row {y}: {mismatch_report(img1[y:y+1], ref[y:y+1])}"
+
+
+def test_headline_properties(headline):
+    case, img1, img1b, img2, lit, st = headline
+    assert np.array_equal(img1, img1b)           # deterministic
+    assert not np.array_equal(img1, img2)        # rng_offset changes the frame
+    assert np.array_equal(img1, lit)             # tuned == literal at full size
+    assert (img1[..., 3] == 255).all()
+    n = 1920 * 1080 * 64
+    assert n <= st.segments <= 9 * n             # every path: 1..max_bounces+1 segments
+    assert st.tri_tests <= st.segments * 1610
