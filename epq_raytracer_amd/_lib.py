@@ -61,7 +61,7 @@ class Layout(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("segments", c_uint64), ("tri_tests", c_uint64), ("traces", c_uint64), ("accumulates", c_uint64),
-                ("last_trace_ms", c_float), ("total_trace_ms", c_float)]
+                ("last_trace_ms", c_float), ("total_trace_ms", c_float), ("wave_steps", c_uint64)]
 
 
 HRT_OK = 0

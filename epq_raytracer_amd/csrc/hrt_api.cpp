@@ -28,6 +28,7 @@ static_assert(offsetof(hrt_push_constants, height) == 120, "push layout");
 namespace {
 
 thread_local std::string g_create_error;
+constexpr int kNumCounters = 3;  // segments, triangle tests, wave steps
 
 struct EventPair {
   hipEvent_t start = nullptr, stop = nullptr;
@@ -177,9 +178,9 @@ extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_
     if ((e = hipMalloc((void**)&ctx->accum32, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(accum)"));
   }
   if ((e = hipMalloc(&ctx->scratch, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(scratch)"));
-  if ((e = hipMalloc((void**)&ctx->counters, 2 * sizeof(unsigned long long))) != hipSuccess)
+  if ((e = hipMalloc((void**)&ctx->counters, kNumCounters * sizeof(unsigned long long))) != hipSuccess)
     return bail(hip_fail(ctx, e, "hipMalloc(counters)"));
-  if ((e = hipMemsetAsync(ctx->counters, 0, 2 * sizeof(unsigned long long), ctx->stream)) != hipSuccess)
+  if ((e = hipMemsetAsync(ctx->counters, 0, kNumCounters * sizeof(unsigned long long), ctx->stream)) != hipSuccess)
     return bail(hip_fail(ctx, e, "hipMemset(counters)"));
   // Fresh images read as the cleared state (0,0,0,1) until the first dispatch writes them.
   if ((e = hrt::launch_clear(ctx->trace8, ctx->trace32, np, ctx->stream)) != hipSuccess)
@@ -288,6 +289,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.row_tile = ctx->row_tile;
   p.part_index = ctx->part_index;
   p.part_count = ctx->part_count;
+  p.n_tris = ctx->n_tris;
   // The fused-loop variant assumes max_bounces >= 0 (a negative count traces no segment at all).
   const int variant = pc->max_bounces < 0 ? 1 : ctx->variant;
 
@@ -382,12 +384,13 @@ extern "C" hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out) {
   hrt_status st = hrt_synchronize(ctx);
   if (st != HRT_OK) return st;
   if ((st = harvest_events(ctx)) != HRT_OK) return st;
-  unsigned long long c[2] = {0, 0};
+  unsigned long long c[kNumCounters] = {0, 0, 0};
   HRT_HIP(ctx, hipMemcpy(c, ctx->counters, sizeof c, hipMemcpyDeviceToHost));
   out->segments = c[0];
   out->tri_tests = c[1];
   out->traces = ctx->traces;
   out->accumulates = ctx->accumulates;
+  out->wave_steps = c[2];
   out->last_trace_ms = ctx->last_ms;
   out->total_trace_ms = ctx->total_ms;
   return HRT_OK;
@@ -398,7 +401,7 @@ extern "C" hrt_status hrt_reset_stats(hrt_context* ctx) {
   hrt_status st = hrt_synchronize(ctx);
   if (st != HRT_OK) return st;
   if ((st = harvest_events(ctx)) != HRT_OK) return st;
-  HRT_HIP(ctx, hipMemsetAsync(ctx->counters, 0, 2 * sizeof(unsigned long long), ctx->stream));
+  HRT_HIP(ctx, hipMemsetAsync(ctx->counters, 0, kNumCounters * sizeof(unsigned long long), ctx->stream));
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->traces = ctx->accumulates = 0;
   ctx->last_ms = ctx->total_ms = 0.0f;
@@ -409,7 +412,7 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   switch (key) {
     case HRT_OPT_KERNEL_VARIANT:
-      if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be 0 or 1");
+      if (value < 0 || value > 7) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be in [0, 7]");
       ctx->variant = (int)value;
       return HRT_OK;
     case HRT_OPT_COUNTERS:

@@ -19,6 +19,7 @@ struct TraceParams {
   unsigned long long* counters;  // [0] segments, [1] triangle tests; nullptr = off
   hrt_push_constants pc;
   uint32_t local_rows, row_tile, part_index, part_count;
+  uint32_t n_tris;               // uploaded triangle count (LDS staging)
 };
 
 hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream);

@@ -214,18 +214,21 @@ __device__ __forceinline__ void store_pixel(const TraceParams& P, uint32_t x, ui
   if (P.img32) P.img32[idx] = make_float4(col.x, col.y, col.z, 1.0f);
 }
 
-// wave-level sum of the per-lane counters, one 64-bit atomic per wave.
+// wave-level sums of the per-lane counters (+ the wave's longest lane), one atomic each per wave.
 __device__ __forceinline__ void flush_counters(const TraceParams& P, uint32_t segs, uint32_t tests) {
   if (!P.counters) return;
   unsigned long long s = segs, t = tests;
+  uint32_t mx = segs;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     s += __shfl_xor(s, off, 64);
     t += __shfl_xor(t, off, 64);
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
   }
   if ((threadIdx.x & 63) == 0) {
     atomicAdd(&P.counters[0], s);
     atomicAdd(&P.counters[1], t);
+    atomicAdd(&P.counters[2], (unsigned long long)mx);
   }
 }
 
@@ -276,43 +279,154 @@ __global__ __launch_bounds__(256) void trace_literal(TraceParams P) {
 //   R5  RN(num_u - num_v) > RN(det * (1+2^-16))   (then w = 1-u-v < 0)
 //   R7  num_t >  RN(best_k * det), best_k = RN(best * (1+2^-16))   (then dist >= best)
 // A lane that passes the pre-test is only a candidate; the exact reference expression decides.
-__device__ __forceinline__ void tri_tuned(const hrt_triangle& tri, uint32_t i, uint32_t m, f3 o, f3 d,
-                                          Closest& c, float& best_k) {
-  const f3 n = ld3(tri.normal);
+constexpr float kTiny = 8.673617379884035e-19f;   // 2^-60
+constexpr float kOnePlus = 1.0000152587890625f;   // 1 + 2^-16
+constexpr float kTMin = 0.000999f;
+
+// Division-free part of one triangle test for one lane (all quantities exactly as the reference
+// computes them, so the exact path below can reuse them).
+struct TriPre {
+  float num_t, num_u, num_v, det;
+  bool cand;
+};
+
+// The 12 floats of a triangle record the test reads.
+struct TriData {
+  f3 a, e1, e2, n;
+};
+
+// Triangle sources: the std430 buffer read with wave-uniform addresses (-> SGPRs), or the LDS copy.
+struct GlobalTris {
+  const hrt_triangle* __restrict__ t;
+  __device__ __forceinline__ TriData operator()(uint32_t i) const {
+    const hrt_triangle& r = t[i];
+    return {ld3(r.a), ld3(r.edge_one), ld3(r.edge_two), ld3(r.normal)};
+  }
+};
+struct GlobalTris4 {  // whole 64-byte records (lets hipcc use wide s_loads)
+  const float4* __restrict__ t;
+  __device__ __forceinline__ TriData operator()(uint32_t i) const {
+    const float4 A = t[4 * i], B = t[4 * i + 1], C = t[4 * i + 2], N = t[4 * i + 3];
+    return {mk(A.x, A.y, A.z), mk(B.x, B.y, B.z), mk(C.x, C.y, C.z), mk(N.x, N.y, N.z)};
+  }
+};
+// LDS image: 3 float4 per triangle = (a.xyz, n.x) (n.yz, e1.xy) (e1.z, e2.xyz)
+struct LdsTris {
+  const float4* t;
+  __device__ __forceinline__ TriData operator()(uint32_t i) const {
+    const float4 p = t[3 * i], q = t[3 * i + 1], r = t[3 * i + 2];
+    return {mk(p.x, p.y, p.z), mk(q.z, q.w, r.x), mk(r.y, r.z, r.w), mk(p.w, q.x, q.y)};
+  }
+};
+
+__device__ __forceinline__ TriPre tri_pre(const TriData& tri, f3 o, f3 d, float best_k) {
+  TriPre r;
+  const f3 n = tri.n;
   const float dn = dot(d, n);
-  const f3 ao = o - ld3(tri.a);
-  const float num_t = dot(ao, n);
+  const f3 ao = o - tri.a;
+  r.num_t = dot(ao, n);
   const f3 dao = cross(ao, d);
-  const float num_u = dot(ld3(tri.edge_two), dao);
-  const float num_v = dot(ld3(tri.edge_one), dao);
-  const float det = -dn;
-  const float tiny = det * 8.673617379884035e-19f;  // det * 2^-60
-  const bool reject = (num_t < det * 0.000999f) | (num_u < -tiny) | (num_v > tiny) |
-                      ((num_u - num_v) > det * 1.0000152587890625f) | (num_t > best_k * det);
-  const bool cand = (dn < 0.0f) & (!reject | (det < 8.673617379884035e-19f));
-  if (__builtin_expect(__any(cand), 0)) {
-    if (cand) {
-      const float inv_det = 1.0f / det;
-      const float dist = num_t * inv_det;
-      const float u = num_u * inv_det;
-      const float v = -num_v * inv_det;
-      const float w = 1.0f - u - v;
-      if (!(dist < 0.0f) && !(u < 0.0f) && !(v < 0.0f) && !(w < 0.0f) && dist > 0.001f && dist < c.t) {
-        c = Closest{dist, 2, i, m};
-        best_k = dist * 1.0000152587890625f;
+  r.num_u = dot(tri.e2, dao);
+  r.num_v = dot(tri.e1, dao);
+  r.det = -dn;
+  const float tiny = r.det * kTiny;
+  const bool reject = (r.num_t < r.det * kTMin) | (r.num_u < -tiny) | (r.num_v > tiny) |
+                      ((r.num_u - r.num_v) > r.det * kOnePlus) | (r.num_t > best_k * r.det);
+  r.cand = (dn < 0.0f) & (!reject | (r.det < kTiny));
+  return r;
+}
+
+// The reference's remaining arithmetic (raytracing.glsl:227-238) for a candidate lane.
+__device__ __forceinline__ void tri_exact(const TriPre& q, uint32_t i, uint32_t m, Closest& c, float& best_k) {
+  const float inv_det = 1.0f / q.det;
+  const float dist = q.num_t * inv_det;
+  const float u = q.num_u * inv_det;
+  const float v = -q.num_v * inv_det;
+  const float w = 1.0f - u - v;
+  if (!(dist < 0.0f) && !(u < 0.0f) && !(v < 0.0f) && !(w < 0.0f) && dist > 0.001f && dist < c.t) {
+    c = Closest{dist, 2, i, m};
+    best_k = dist * kOnePlus;
+  }
+}
+
+// G consecutive triangles: G pre-tests, then one wave-uniform branch into the exact path.  Within
+// the group the exact tests run in buffer order against the updated closest hit (ties: first wins);
+// best_k is only tightened between groups, which keeps the pre-test conservative.
+template <int G, class Src>
+__device__ __forceinline__ void tri_group(const Src& tris, uint32_t i0, uint32_t m, f3 o, f3 d,
+                                          Closest& c, float& best_k) {
+  TriPre q[G];
+  bool any = false;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    q[g] = tri_pre(tris(i0 + g), o, d, best_k);
+    any |= q[g].cand;
+  }
+  if (__builtin_expect(__any(any), 0)) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (G == 1 || __any(q[g].cand)) {
+        if (q[g].cand) tri_exact(q[g], i0 + g, m, c, best_k);
       }
     }
   }
 }
 
-__device__ __forceinline__ Closest world_hit_tuned(const Scene& sc, const hrt_push_constants& pc, f3 o, f3 d,
-                                                   uint32_t& tests) {
+// Two-stage variant: stage 1 computes only ao and num_t (7 VALU) and skips the triangle when no
+// lane has num_t > 0 (necessary for dist > 0.001 since inv_det > 0).  For primary rays all lanes share
+// the origin, so num_t is wave-uniform and every triangle facing away from the camera is rejected
+// here; stage 2 completes the same pre-test as tri_pre.
+template <class Src>
+__device__ __forceinline__ void tri_two_stage(const Src& tris, uint32_t i, uint32_t m, f3 o, f3 d, Closest& c,
+                                              float& best_k) {
+  const TriData tri = tris(i);
+  const f3 ao = o - tri.a;
+  TriPre q;
+  q.num_t = dot(ao, tri.n);
+  if (!__any(q.num_t > 0.0f)) return;
+  const float dn = dot(d, tri.n);
+  const f3 dao = cross(ao, d);
+  q.num_u = dot(tri.e2, dao);
+  q.num_v = dot(tri.e1, dao);
+  q.det = -dn;
+  const float tiny = q.det * kTiny;
+  const bool reject = (q.num_t < q.det * kTMin) | (q.num_u < -tiny) | (q.num_v > tiny) |
+                      ((q.num_u - q.num_v) > q.det * kOnePlus) | (q.num_t > best_k * q.det);
+  q.cand = (dn < 0.0f) & (q.num_t > 0.0f) & (!reject | (q.det < kTiny));
+  if (__builtin_expect(__any(q.cand), 0)) {
+    if (q.cand) tri_exact(q, i, m, c, best_k);
+  }
+}
+
+template <class Src>
+__device__ __forceinline__ Closest world_hit_two_stage(const Scene& sc, const Src& src, const hrt_push_constants& pc,
+                                                       f3 o, f3 d, uint32_t& tests) {
   Closest c{kFltMax, 0, 0u, 0u};
   for (int i = 0; i < pc.num_spheres; ++i) {
     const float t = sphere_dist(sc.spheres[i], o, d);
     if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
   }
-  float best_k = c.t * 1.0000152587890625f;  // FLT_MAX*(1+2^-16) = inf: R7 never rejects
+  float best_k = c.t * kOnePlus;
+  for (int m = 0; m < pc.num_meshes; ++m) {
+    const hrt_mesh& mesh = sc.meshes[m];
+    const bool pass = aabb_pass(mesh, o, d);
+    tests += pass ? mesh.len : 0u;
+    if (!pass) continue;
+    const uint32_t end = mesh.first_index + mesh.len;
+    for (uint32_t i = mesh.first_index; i < end; ++i) tri_two_stage(src, i, (uint32_t)m, o, d, c, best_k);
+  }
+  return c;
+}
+
+template <int G, class Src>
+__device__ __forceinline__ Closest world_hit_tuned(const Scene& sc, const Src& src, const hrt_push_constants& pc,
+                                                   f3 o, f3 d, uint32_t& tests) {
+  Closest c{kFltMax, 0, 0u, 0u};
+  for (int i = 0; i < pc.num_spheres; ++i) {
+    const float t = sphere_dist(sc.spheres[i], o, d);
+    if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
+  }
+  float best_k = c.t * kOnePlus;  // FLT_MAX*(1+2^-16) = inf: R7 never rejects
   for (int m = 0; m < pc.num_meshes; ++m) {
     const hrt_mesh& mesh = sc.meshes[m];
     const bool pass = aabb_pass(mesh, o, d);
@@ -320,8 +434,9 @@ __device__ __forceinline__ Closest world_hit_tuned(const Scene& sc, const hrt_pu
     if (!pass) continue;
     const uint32_t end = mesh.first_index + mesh.len;
     uint32_t i = mesh.first_index;
-#pragma unroll 2
-    for (; i < end; ++i) tri_tuned(sc.tris[i], i, (uint32_t)m, o, d, c, best_k);
+    for (; i + G <= end; i += G) tri_group<G, Src>(src, i, (uint32_t)m, o, d, c, best_k);
+    if (G > 1)
+      for (; i < end; ++i) tri_group<1, Src>(src, i, (uint32_t)m, o, d, c, best_k);
   }
   return c;
 }
@@ -329,11 +444,10 @@ __device__ __forceinline__ Closest world_hit_tuned(const Scene& sc, const hrt_pu
 // Fused sample/bounce loop: each lane runs its pixel's num_samples paths back to back
 // (RNG state chains through them exactly as raytracing.glsl:379-385); the wave iterates until
 // every lane's last path has ended.
-__global__ __launch_bounds__(256) void trace_tuned(TraceParams P) {
+template <int G, class Src, bool TwoStage = false>
+__device__ __forceinline__ void trace_fused(const TraceParams& P, const Src& src, uint32_t x, uint32_t lr) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
-  uint32_t x, lr;
-  lane_pixel(P, x, lr);
   const uint32_t y = global_row(lr, P);
   uint32_t segs = 0, tests = 0;
   const bool active = x < pc.width && lr < P.local_rows && y < pc.height;
@@ -354,7 +468,8 @@ __global__ __launch_bounds__(256) void trace_tuned(TraceParams P) {
         const f3 dir = get_ray_dir(pc, centre, state);
         p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, normalize(dir), 0, true};
       }
-      const Closest c = world_hit_tuned(sc, pc, p.pos, p.dir, tests);
+      const Closest c = TwoStage ? world_hit_two_stage(sc, src, pc, p.pos, p.dir, tests)
+                                 : world_hit_tuned<G>(sc, src, pc, p.pos, p.dir, tests);
       ++segs;
       const bool ended = shade_step(sc, pc, p, c, state);
       ++p.bounce;
@@ -367,6 +482,48 @@ __global__ __launch_bounds__(256) void trace_tuned(TraceParams P) {
     store_pixel(P, x, lr, colour);
   }
   flush_counters(P, segs, tests);
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void trace_tuned(TraceParams P) {
+  uint32_t x, lr;
+  lane_pixel(P, x, lr);
+  trace_fused<G>(P, GlobalTris{P.tris}, x, lr);
+}
+
+__global__ __launch_bounds__(256) void trace_tuned_f4(TraceParams P) {
+  uint32_t x, lr;
+  lane_pixel(P, x, lr);
+  trace_fused<1>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr);
+}
+
+// Whole scene resident in LDS (3 float4 per triangle), 1024-thread workgroups (16 waves, a 32x32
+// pixel tile of 8x8 wave tiles): the copy is paid once per workgroup, every wave then streams the
+// triangles from LDS with broadcast reads instead of scalar loads.
+extern __shared__ float4 lds_tris[];
+template <bool TwoStage>
+__global__ __launch_bounds__(1024) void trace_lds(TraceParams P) {
+  const uint32_t n = P.n_tris;
+  for (uint32_t k = threadIdx.x; k < 3 * n; k += blockDim.x) {
+    const uint32_t i = k / 3, part = k - 3 * i;
+    const hrt_triangle& t = P.tris[i];
+    float4 v;
+    if (part == 0) v = make_float4(t.a[0], t.a[1], t.a[2], t.normal[0]);
+    else if (part == 1) v = make_float4(t.normal[1], t.normal[2], t.edge_one[0], t.edge_one[1]);
+    else v = make_float4(t.edge_one[2], t.edge_two[0], t.edge_two[1], t.edge_two[2]);
+    lds_tris[k] = v;
+  }
+  __syncthreads();
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t x = blockIdx.x * 32 + (wave & 3) * 8 + (lane & 7);
+  const uint32_t lr = blockIdx.y * 32 + (wave >> 2) * 8 + (lane >> 3);
+  trace_fused<1, LdsTris, TwoStage>(P, LdsTris{lds_tris}, x, lr);
+}
+
+__global__ __launch_bounds__(256) void trace_two_stage_f4(TraceParams P) {
+  uint32_t x, lr;
+  lane_pixel(P, x, lr);
+  trace_fused<1, GlobalTris4, true>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr);
 }
 
 // ---- init clear (raytracing.glsl:363-366) and image_combiner.glsl (:22-43) ----------------------
@@ -429,13 +586,37 @@ __global__ __launch_bounds__(256) void f32_to_rgba8(const float4* src, uint32_t*
 namespace hrt {
 
 static inline unsigned blocks_for(size_t n) { return (unsigned)((n + 255) / 256); }
+constexpr size_t kMaxLdsScene = 160 * 1024;
 
 hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream) {
+  static bool lds_attr = false;
+  if (!lds_attr) {
+    lds_attr = true;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_lds<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_lds<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
+  }
   const dim3 grid((p.pc.width + 15) / 16, (p.local_rows + 15) / 16, 1);
-  if (variant == 1)
-    trace_literal<<<grid, 256, 0, stream>>>(p);
-  else
-    trace_tuned<<<grid, 256, 0, stream>>>(p);
+  const size_t lds_bytes = (size_t)p.n_tris * 48;
+  if (variant == 0) variant = 6;  // auto: two-stage test, scene in LDS when it fits
+  if ((variant == 5 || variant == 6) && lds_bytes > kMaxLdsScene) variant = (variant == 6) ? 7 : 3;
+  switch (variant) {
+    case 1: trace_literal<<<grid, 256, 0, stream>>>(p); break;
+    case 3: trace_tuned_f4<<<grid, 256, 0, stream>>>(p); break;
+    case 4: trace_tuned<2><<<grid, 256, 0, stream>>>(p); break;
+    case 5:
+    case 6: {
+      const dim3 g32((p.pc.width + 31) / 32, (p.local_rows + 31) / 32, 1);
+      if (variant == 5)
+        trace_lds<false><<<g32, 1024, lds_bytes, stream>>>(p);
+      else
+        trace_lds<true><<<g32, 1024, lds_bytes, stream>>>(p);
+      break;
+    }
+    case 7: trace_two_stage_f4<<<grid, 256, 0, stream>>>(p); break;
+    default: trace_tuned<1><<<grid, 256, 0, stream>>>(p); break;  // 2
+  }
   return hipGetLastError();
 }
 

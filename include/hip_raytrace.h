@@ -141,6 +141,8 @@ typedef struct hrt_stats {
   uint64_t accumulates;   /* combiner dispatches since reset */
   float last_trace_ms;    /* device time of the last trace dispatch (HIP events) */
   float total_trace_ms;   /* device time of all trace dispatches since reset */
+  uint64_t wave_steps;    /* sum over waves of the wave's longest per-lane segment count: lane
+                             efficiency = segments / (64 * wave_steps) */
 } hrt_stats;
 
 typedef struct hrt_context hrt_context;

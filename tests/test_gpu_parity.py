@@ -13,7 +13,8 @@ from helpers import E, SceneCase, _lib, mismatch_report
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1]  # tuned, literal
+VARIANTS = [0, 1]  # auto (tuned), literal
+ALL_VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7]  # every kernel variant (hrt_set_option HRT_OPT_KERNEL_VARIANT)
 
 CONFIGS = [
     # (scene, size, spp, bounces, rng_offset)
@@ -35,6 +36,17 @@ CONFIGS = [
 @pytest.mark.parametrize("scene,size,spp,bounces,off", CONFIGS)
 def test_frame_bit_exact(scene, size, spp, bounces, off, variant):
     case = SceneCase(scene, size, spp, bounces, rng_offset=off)
+    ref, _, seg, tt = case.oracle()
+    img, gseg, gtt = case.gpu(variant=variant)
+    assert np.array_equal(img, ref), mismatch_report(img, ref)
+    assert (gseg, gtt) == (seg, tt)
+
+
+@pytest.mark.parametrize("variant", ALL_VARIANTS)
+@pytest.mark.parametrize("scene,size,spp,bounces", [("island", (96, 64), 4, 8), ("cave", (64, 48), 2, 8),
+                                                    ("box", (45, 33), 3, 6), ("spheres", (40, 30), 2, 8)])
+def test_every_variant_bit_exact(scene, size, spp, bounces, variant):
+    case = SceneCase(scene, size, spp, bounces)
     ref, _, seg, tt = case.oracle()
     img, gseg, gtt = case.gpu(variant=variant)
     assert np.array_equal(img, ref), mismatch_report(img, ref)
@@ -162,7 +174,7 @@ def test_triangle_soup(n):
     case = SceneCase(settings=st, camera=E.Camera([0.0, 0.0, -25.0], [0.0, 0.0, 1.0]), size=(96, 96),
                      num_samples=2, max_bounces=6)
     ref, _, seg, tt = case.oracle()
-    for variant in VARIANTS:
+    for variant in ALL_VARIANTS:
         img, gseg, gtt = case.gpu(variant=variant)
         assert np.array_equal(img, ref), mismatch_report(img, ref)
         assert (gseg, gtt) == (seg, tt)
@@ -199,7 +211,7 @@ def test_degenerate_and_adversarial_geometry():
     case = SceneCase(settings=st, camera=E.Camera([0.1, 0.2, -6.0], [0.0, 0.0, 1.0]), size=(128, 128),
                      num_samples=3, max_bounces=8)
     ref, _, seg, tt = case.oracle()
-    for variant in VARIANTS:
+    for variant in ALL_VARIANTS:
         img, gseg, gtt = case.gpu(variant=variant)
         assert np.array_equal(img, ref), mismatch_report(img, ref)
         assert (gseg, gtt) == (seg, tt)

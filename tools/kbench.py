@@ -1,0 +1,71 @@
+"""Kernel A/B on the GPU box: trace variants interleaved in ONE process (cdna guide rule 24).
+
+    python tools/kbench.py --variants 1 2 3 4 --rounds 3 [--scene island --size 1920x1080 --spp 64 --bounces 8]
+
+Prints, per variant: median / min kernel ms (HIP events), Mrays/s, algorithmic TFLOP/s (38 FLOP per
+reference triangle test), lane efficiency (segments / (64 * wave steps)) and whether the frame is
+byte-identical to variant 1 (literal).
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
+
+from helpers import SceneCase, _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", type=int, nargs="+", default=[1, 2, 3, 4])
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--scene", default="island")
+    ap.add_argument("--size", default="1920x1080")
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    W, H = (int(v) for v in a.size.split("x"))
+    case = SceneCase(a.scene, (W, H), a.spp, a.bounces)
+    ctx = case.context()
+    pc = case.push(1)
+    # warm up + reference image
+    ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
+    ctx.trace(pc)
+    ref = ctx.read(_lib.IMG_TRACE)
+    res = {v: [] for v in a.variants}
+    stats = {}
+    same = {}
+    for r in range(a.rounds):
+        for v in a.variants:
+            ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
+            ctx.reset_stats()
+            ctx.trace(pc)
+            st = ctx.stats()
+            res[v].append(st.total_trace_ms)
+            stats[v] = (st.segments, st.tri_tests, st.wave_steps)
+            if r == 0:
+                same[v] = bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
+    out = []
+    for v in a.variants:
+        ms = np.array(res[v])
+        seg, tt, ws = stats[v]
+        med = float(np.median(ms))
+        row = {"variant": v, "ms_median": round(med, 3), "ms_min": round(float(ms.min()), 3),
+               "mrays_s": round(seg / med / 1e3, 1), "tflops_alg": round(38 * tt / med / 1e9, 2),
+               "lane_eff": round(seg / max(64 * ws, 1), 4), "segments": seg, "tri_tests": tt,
+               "identical_to_literal": same[v]}
+        out.append(row)
+        print(json.dumps(row), flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"workload": vars(a), "results": out}, f, indent=1)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
