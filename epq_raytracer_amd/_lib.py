@@ -70,7 +70,7 @@ STATUS_NAMES = {0: "HRT_OK", 1: "HRT_ERR_INVALID_ARGUMENT", 2: "HRT_ERR_NO_DEVIC
 MODE_RGBA8, MODE_RGBA32F = 0, 1
 IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
-OPT_KERNEL_VARIANT, OPT_COUNTERS = 1, 2
+OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH = 1, 2, 3
 
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).
 EXPORTED_SYMBOLS = (

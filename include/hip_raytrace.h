@@ -152,7 +152,10 @@ typedef enum hrt_option {
   /* kernel variant: 0 = tuned (default), 1 = literal per-sample loop (same results, A/B and parity) */
   HRT_OPT_KERNEL_VARIANT = 1,
   /* 1 = count segments / triangle tests on the device (default 1; 0 removes the counters' cost) */
-  HRT_OPT_COUNTERS = 2
+  HRT_OPT_COUNTERS = 2,
+  /* bundle kernel: a wave runs its bounce (non-primary) segments once this many lanes wait for one,
+   * or when no lane has a primary segment left (1..64, default 48; results do not depend on it) */
+  HRT_OPT_SECONDARY_BATCH = 3
 } hrt_option;
 
 uint32_t hrt_abi_version(void);

@@ -1,12 +1,17 @@
 #!/bin/bash
-# One GPU-box session: smoke, bench (N=1), rocprofv3 kernel-trace summary of the same bench.
-# Usage (from the repo root, via gpurun): bash tools/gpu_round.sh <tag> [bench args...]
+# One GPU-box session: GPU tests, smoke, bench (N=1), rocprofv3 kernel-trace summary of the same bench,
+# PMC passes (traffic + executed FLOPs).  Usage (repo root, via gpurun): bash tools/gpu_round.sh <tag>
 set -o pipefail
 TAG=${1:-r01}; shift
-mkdir -p gpurun_out/$TAG
+OUT=gpurun_out/$TAG; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$TAG/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/$TAG/smoke.log; exit 1; }
-timeout -k 10 600 python3 bench.py "$@" > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || { echo "bench failed"; tail -30 gpurun_out/$TAG/bench.err; exit 1; }
-cat gpurun_out/$TAG/bench.json
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG/prof -o run --output-format csv -- python3 bench.py --cpu-seconds 0 "$@" > gpurun_out/$TAG/prof.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/$TAG/prof.log; exit 1; }
-find gpurun_out/$TAG/prof -name '*kernel_stats.csv' -exec cat {} \;
+timeout -k 10 900 python3 -m pytest tests -m gpu -q > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 $OUT/gpu_tests.log; exit 1; }
+tail -2 $OUT/gpu_tests.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; cat $OUT/smoke.log; exit 1; }
+cat $OUT/smoke.log
+bash tools/pmc.sh $TAG/pmc 0 > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $OUT/pmc.log; exit 1; }
+cp $OUT/pmc/pmc_traffic.json profiles/pmc_traffic.json
+timeout -k 10 600 python3 bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --cpu-seconds 0 "$@" > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
+find $OUT/prof -name '*kernel_stats.csv' -exec cat {} \;

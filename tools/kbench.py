@@ -28,37 +28,43 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--no-ref", action="store_true", help="skip the literal-kernel reference frame")
+    ap.add_argument("--sec-batch", type=int, nargs="+", default=[48], help="HRT_OPT_SECONDARY_BATCH values to sweep")
     a = ap.parse_args()
     W, H = (int(v) for v in a.size.split("x"))
     case = SceneCase(a.scene, (W, H), a.spp, a.bounces)
     ctx = case.context()
     pc = case.push(1)
-    # warm up + reference image
-    ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
-    ctx.trace(pc)
-    ref = ctx.read(_lib.IMG_TRACE)
-    res = {v: [] for v in a.variants}
+    # warm up + reference image (literal kernel), unless profiling one variant alone
+    ref = None
+    if not a.no_ref:
+        ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
+        ctx.trace(pc)
+        ref = ctx.read(_lib.IMG_TRACE)
+    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v >= 14 else [a.sec_batch[0]])]
+    res = {vs: [] for vs in combos}
     stats = {}
     same = {}
     for r in range(a.rounds):
-        for v in a.variants:
+        for v, sb in combos:
             ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
+            ctx.set_option(_lib.OPT_SECONDARY_BATCH, sb)
             ctx.reset_stats()
             ctx.trace(pc)
             st = ctx.stats()
-            res[v].append(st.total_trace_ms)
-            stats[v] = (st.segments, st.tri_tests, st.wave_steps)
+            res[(v, sb)].append(st.total_trace_ms)
+            stats[(v, sb)] = (st.segments, st.tri_tests, st.wave_steps)
             if r == 0:
-                same[v] = bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
+                same[(v, sb)] = None if ref is None else bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
     out = []
-    for v in a.variants:
-        ms = np.array(res[v])
-        seg, tt, ws = stats[v]
+    for v, sb in combos:
+        ms = np.array(res[(v, sb)])
+        seg, tt, ws = stats[(v, sb)]
         med = float(np.median(ms))
-        row = {"variant": v, "ms_median": round(med, 3), "ms_min": round(float(ms.min()), 3),
+        row = {"variant": v, "sec_batch": sb, "ms_median": round(med, 3), "ms_min": round(float(ms.min()), 3),
                "mrays_s": round(seg / med / 1e3, 1), "tflops_alg": round(38 * tt / med / 1e9, 2),
                "lane_eff": round(seg / max(64 * ws, 1), 4), "segments": seg, "tri_tests": tt,
-               "identical_to_literal": same[v]}
+               "identical_to_literal": same[(v, sb)]}
         out.append(row)
         print(json.dumps(row), flush=True)
     if a.json:
