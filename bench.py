@@ -28,6 +28,8 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
 FLOP_PER_TEST = 38         # algorithmic fp32 FLOP per ray-triangle test (raytracing.glsl:213-241)
 BYTES_PER_PIXEL_FRAME = 32  # 16 B ray centre + 4 B trace store + 12 B combiner (r, r, w)
+KERNEL_SYMBOLS = {0: "hrt::trace_bundle_cull", 1: "hrt::trace_literal", 2: "hrt::trace_brute",
+                  3: "hrt::trace_brute_lds", 4: "hrt::trace_bundle", 5: "hrt::trace_bundle_cull"}
 
 
 def parse():
@@ -40,7 +42,8 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=64, help="samples per pixel per frame (num_samples)")
     ap.add_argument("--bounces", type=int, default=8, help="max_bounces")
-    ap.add_argument("--variant", type=int, default=0, help="0 tuned, 1 literal")
+    ap.add_argument("--variant", type=int, default=0,
+                    help="hrt_kernel: 0 auto, 1 literal, 2 brute, 3 brute_lds, 4 bundle, 5 bundle_cull")
     ap.add_argument("--row-tile", type=int, default=16)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo = host-staged gather (rehearsal on one GPU)")
@@ -174,7 +177,7 @@ def main():
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                        "parallelism": (f"row-tiles{world}x{args.row_tile} ({args.dist_backend} gather)"
                                        if dist_on else "single-gpu"),
-                       "kernel_variant": "tuned" if args.variant == 0 else "literal"},
+                       "kernel_variant": _lib.KERNEL_NAMES[args.variant]},
             "segments_per_step": segs_all // args.steps,
             "tri_tests_per_step": tests_all // args.steps,
             "paths_per_s": W * H * args.spp / (elapsed / args.steps),
@@ -184,7 +187,7 @@ def main():
                          "achieved_basis": "executed (rocprofv3 PMC FLOP count per launch / live launch time)"
                                            if executed_flops else "reference-equivalent (38 FLOP x reference tests)",
                          "algorithmic_tflops": round(algorithmic_tf, 3),
-                         "kernel": "hrt::trace_bundle" if args.variant in (0, 14) else f"variant {args.variant}",
+                         "kernel": KERNEL_SYMBOLS[args.variant],
                          "kernel_ms": round(kern_ms, 3), "flop_per_test": FLOP_PER_TEST,
                          "tests_per_launch": int(tests_per_launch), "pmc_source": pmc_note},
             "hbm_roofline": {"achieved": round(algo_bytes / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,

@@ -71,6 +71,9 @@ MODE_RGBA8, MODE_RGBA32F = 0, 1
 IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH = 1, 2, 3
+# hrt_kernel (include/hip_raytrace.h)
+KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
+KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull"}
 
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).
 EXPORTED_SYMBOLS = (

@@ -55,11 +55,10 @@ struct hrt_context {
   float4* accum32 = nullptr;
   void* scratch = nullptr;  // format conversion for hrt_read_image
   unsigned long long* counters = nullptr;
-  uint32_t* cam_list = nullptr;   // camera-facing lists (per-frame prep of variant 8/9)
-  uint32_t* cam_meta = nullptr;   // cam_start[n_meshes], cam_count[n_meshes]
-  uint32_t cam_capacity = 0;
-  float4* cam_tris = nullptr;     // compacted camera-facing records (variant 10)
-  float4* cam_cull = nullptr;     // bundle-cull records (variant 14)
+  uint32_t* cam_meta = nullptr;   // bundle variants: cam_start[n_meshes], cam_count[n_meshes]
+  uint32_t cam_capacity = 0;      // sum of mesh lengths
+  float4* cam_tris = nullptr;     // compacted camera-facing records (64 B each)
+  float4* cam_cull = nullptr;     // bundle-cull records (80 B each)
 
   int variant = 0;
   bool counters_on = true;
@@ -212,7 +211,6 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
   free_dev(ctx->accum32);
   free_dev(ctx->scratch);
   free_dev(ctx->counters);
-  free_dev(ctx->cam_list);
   free_dev(ctx->cam_meta);
   free_dev(ctx->cam_tris);
   free_dev(ctx->cam_cull);
@@ -265,14 +263,12 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   uint64_t cap = 0;
   for (uint32_t m = 0; m < n_meshes; ++m) cap += meshes[m].len;
   if (cap > 0xFFFFFFFFull) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_set_scene: too many mesh triangles");
-  free_dev(ctx->cam_list);
+  // bundle-variant buffers: per-frame compacted camera-facing records (filled by camera_lists)
   free_dev(ctx->cam_meta);
   free_dev(ctx->cam_tris);
-  HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_list, (size_t)(cap ? cap : 1) * 4));
-  HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_meta, (size_t)(n_meshes ? 2 * n_meshes : 2) * 4));
-  free_dev(ctx->cam_tris);
-  HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_tris, (size_t)(cap ? cap : 1) * 64));
   free_dev(ctx->cam_cull);
+  HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_meta, (size_t)(n_meshes ? 2 * n_meshes : 2) * 4));
+  HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_tris, (size_t)(cap ? cap : 1) * 64));
   HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_cull, (size_t)(cap ? cap : 1) * 80));
   ctx->cam_capacity = (uint32_t)cap;
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
@@ -313,15 +309,13 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.part_index = ctx->part_index;
   p.part_count = ctx->part_count;
   p.n_tris = ctx->n_tris;
-  p.cam_list = ctx->cam_list;
   p.cam_start = ctx->cam_meta;
   p.cam_count = ctx->cam_meta + ctx->n_meshes;
   p.cam_list_capacity = ctx->cam_capacity;
   p.cam_tris = ctx->cam_tris;
   p.cam_cull = ctx->cam_cull;
   p.sec_batch = ctx->sec_batch;
-  // The fused-loop variant assumes max_bounces >= 0 (a negative count traces no segment at all).
-  const int variant = pc->max_bounces < 0 ? 1 : ctx->variant;
+  const int variant = ctx->variant;
 
   EventPair ev;
   if (!ctx->event_pool.empty()) {
@@ -442,7 +436,8 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   switch (key) {
     case HRT_OPT_KERNEL_VARIANT:
-      if (value < 0 || value > 16) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be in [0, 16]");
+      if (value < HRT_KERNEL_AUTO || value > HRT_KERNEL_BUNDLE_CULL)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be an hrt_kernel value (0..5)");
       ctx->variant = (int)value;
       return HRT_OK;
     case HRT_OPT_COUNTERS:

@@ -1,18 +1,22 @@
 // hrt_kernels.hip -- gfx950 kernels for the path-trace dispatch (assets/raytracing.glsl) and the
 // progressive accumulator (assets/image_combiner.glsl).
 //
-// Geometry of a launch: 256-thread workgroups = 4 waves; each wave owns an 8x8 pixel tile (coherent
-// primary rays share triangle-rejection outcomes), a workgroup a 16x16 tile.  Scene records are
-// read with wave-uniform addresses, so hipcc streams triangles through SGPRs (s_load_dwordx16) --
-// every lane of the wave tests the same triangle against its own ray.
+// One lane per pixel; each wave owns an 8x8 pixel tile (coherent primary rays), 256-thread
+// workgroups (1024 for the LDS-resident scene).  Scene records are read with wave-uniform addresses,
+// so triangles stream through SGPRs and every lane tests the same triangle against its own ray.
 //
-// Two trace variants with identical results (tests/test_gpu_parity.py holds both to the oracle):
-//   trace_literal  per-sample / per-bounce loops shaped like raytracing.glsl:308-389;
-//   trace_tuned    the same arithmetic with (a) the sample and bounce loops fused into one
-//                  per-lane segment loop, so a lane whose path ended starts its next sample
-//                  instead of idling until the wave's longest path ends, and (b) a division-free
-//                  conservative pre-test per triangle; the correctly rounded 1/det path runs only
-//                  when some lane of the wave may accept the triangle (DESIGN.md "exact cull").
+// Kernel variants (hrt_option HRT_OPT_KERNEL_VARIANT, include/hip_raytrace.h), all byte-identical
+// to the oracle (tests/test_gpu_parity.py):
+//   LITERAL      per-sample / per-bounce loops shaped like raytracing.glsl:308-389, full test on
+//                every triangle;
+//   BRUTE(_LDS)  the sample and bounce loops fused into one per-lane segment loop (a lane whose path
+//                ended starts its next sample), a division-free exact pre-test per triangle in two
+//                wave-uniform stages; the correctly rounded 1/det path only runs when some lane may
+//                accept (DESIGN.md "exact cull"); triangles via SGPRs or resident in LDS;
+//   BUNDLE       primary segments (origin = cam_pos) rejected 64 triangles at a time by bounding the
+//                reference's linear forms over the wave's ray directions; bounce segments deferred
+//                until a wave has enough of them, then the BRUTE test;
+//   BUNDLE_CULL  BUNDLE + a lane-parallel origin-box / direction-cone pre-cull for bounce segments.
 #include <hip/hip_runtime.h>
 
 #include "hip_raytrace.h"
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(256) void trace_literal(TraceParams P) {
   flush_counters(P, segs, tests);
 }
 
-// ---- tuned variant -----------------------------------------------------------------------------
+// ---- exact pre-test shared by the tuned variants ----------------------------------------------------
 //
 // Exact cull (proof in DESIGN.md): with det = -dot(d,n) > 0 and inv = RN(1/det) > 0, the reference
 // can only accept a triangle if none of these division-free rejections holds (when det >= 2^-60):
@@ -277,63 +281,23 @@ __global__ __launch_bounds__(256) void trace_literal(TraceParams P) {
 //   R3  num_u < -RN(det * 2^-60)              (then u = RN(num_u*inv) < 0, no underflow to -0)
 //   R4  num_v >  RN(det * 2^-60)              (then v < 0)
 //   R5  RN(num_u - num_v) > RN(det * (1+2^-16))   (then w = 1-u-v < 0)
-//   R7  num_t >  RN(best_k * det), best_k = RN(best * (1+2^-16))   (then dist >= best)
+//   R7  num_t >  RN(best_k * det), best_k = RN(best * (1+2^-16))   (then dist > best)
 // A lane that passes the pre-test is only a candidate; the exact reference expression decides.
 constexpr float kTiny = 8.673617379884035e-19f;   // 2^-60
 constexpr float kOnePlus = 1.0000152587890625f;   // 1 + 2^-16
 constexpr float kTMin = 0.000999f;
 
-// Division-free part of one triangle test for one lane (all quantities exactly as the reference
-// computes them, so the exact path below can reuse them).
+// Division-free quantities of one triangle test, computed exactly as the reference does.
 struct TriPre {
   float num_t, num_u, num_v, det;
   bool cand;
 };
 
-// The 12 floats of a triangle record the test reads.
-struct TriData {
-  f3 a, e1, e2, n;
-};
-
-// Triangle sources: the std430 buffer read with wave-uniform addresses (-> SGPRs), or the LDS copy.
-struct GlobalTris {
-  const hrt_triangle* __restrict__ t;
-  __device__ __forceinline__ TriData operator()(uint32_t i) const {
-    const hrt_triangle& r = t[i];
-    return {ld3(r.a), ld3(r.edge_one), ld3(r.edge_two), ld3(r.normal)};
-  }
-};
-struct GlobalTris4 {  // whole 64-byte records (lets hipcc use wide s_loads)
-  const float4* __restrict__ t;
-  __device__ __forceinline__ TriData operator()(uint32_t i) const {
-    const float4 A = t[4 * i], B = t[4 * i + 1], C = t[4 * i + 2], N = t[4 * i + 3];
-    return {mk(A.x, A.y, A.z), mk(B.x, B.y, B.z), mk(C.x, C.y, C.z), mk(N.x, N.y, N.z)};
-  }
-};
-// LDS image: 3 float4 per triangle = (a.xyz, n.x) (n.yz, e1.xy) (e1.z, e2.xyz)
-struct LdsTris {
-  const float4* t;
-  __device__ __forceinline__ TriData operator()(uint32_t i) const {
-    const float4 p = t[3 * i], q = t[3 * i + 1], r = t[3 * i + 2];
-    return {mk(p.x, p.y, p.z), mk(q.z, q.w, r.x), mk(r.y, r.z, r.w), mk(p.w, q.x, q.y)};
-  }
-};
-
-__device__ __forceinline__ TriPre tri_pre(const TriData& tri, f3 o, f3 d, float best_k) {
-  TriPre r;
-  const f3 n = tri.n;
-  const float dn = dot(d, n);
-  const f3 ao = o - tri.a;
-  r.num_t = dot(ao, n);
-  const f3 dao = cross(ao, d);
-  r.num_u = dot(tri.e2, dao);
-  r.num_v = dot(tri.e1, dao);
-  r.det = -dn;
-  const float tiny = r.det * kTiny;
-  const bool reject = (r.num_t < r.det * kTMin) | (r.num_u < -tiny) | (r.num_v > tiny) |
-                      ((r.num_u - r.num_v) > r.det * kOnePlus) | (r.num_t > best_k * r.det);
-  r.cand = (dn < 0.0f) & (!reject | (r.det < kTiny));
-  return r;
+__device__ __forceinline__ bool pre_reject(const TriPre& q, float best_k) {
+  const float tiny = q.det * kTiny;
+  const bool r = (q.num_t < q.det * kTMin) | (q.num_u < -tiny) | (q.num_v > tiny) |
+                 ((q.num_u - q.num_v) > q.det * kOnePlus) | (q.num_t > best_k * q.det);
+  return r & !(q.det < kTiny);
 }
 
 // The reference's remaining arithmetic (raytracing.glsl:227-238) for a candidate lane.
@@ -349,272 +313,54 @@ __device__ __forceinline__ void tri_exact(const TriPre& q, uint32_t i, uint32_t 
   }
 }
 
-// G consecutive triangles: G pre-tests, then one wave-uniform branch into the exact path.  Within
-// the group the exact tests run in buffer order against the updated closest hit (ties: first wins);
-// best_k is only tightened between groups, which keeps the pre-test conservative.
-template <int G, class Src>
-__device__ __forceinline__ void tri_group(const Src& tris, uint32_t i0, uint32_t m, f3 o, f3 d,
-                                          Closest& c, float& best_k) {
-  TriPre q[G];
-  bool any = false;
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    q[g] = tri_pre(tris(i0 + g), o, d, best_k);
-    any |= q[g].cand;
-  }
-  if (__builtin_expect(__any(any), 0)) {
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (G == 1 || __any(q[g].cand)) {
-        if (q[g].cand) tri_exact(q[g], i0 + g, m, c, best_k);
-      }
-    }
-  }
-}
-
-// Two-stage variant: stage 1 computes only ao and num_t (7 VALU) and skips the triangle when no
-// lane has num_t > 0 (necessary for dist > 0.001 since inv_det > 0).  For primary rays all lanes share
-// the origin, so num_t is wave-uniform and every triangle facing away from the camera is rejected
-// here; stage 2 completes the same pre-test as tri_pre.
-template <class Src>
-__device__ __forceinline__ void tri_two_stage(const Src& tris, uint32_t i, uint32_t m, f3 o, f3 d, Closest& c,
-                                              float& best_k) {
-  const TriData tri = tris(i);
-  const f3 ao = o - tri.a;
+// Two-stage test of one triangle record (a, e1, e2, n as float4 with unused w): stage 1 computes
+// ao and num_t and leaves when no lane has num_t > 0 (necessary for dist > 0.001 since inv > 0);
+// stage 2 completes the pre-test.
+__device__ __forceinline__ void tri_two_stage(const float4& A, const float4& B, const float4& C, const float4& N,
+                                              uint32_t i, uint32_t m, f3 o, f3 d, Closest& c, float& best_k) {
+  const f3 n = mk(N.x, N.y, N.z);
+  const f3 ao = o - mk(A.x, A.y, A.z);
   TriPre q;
-  q.num_t = dot(ao, tri.n);
+  q.num_t = dot(ao, n);
   if (!__any(q.num_t > 0.0f)) return;
-  const float dn = dot(d, tri.n);
+  const float dn = dot(d, n);
   const f3 dao = cross(ao, d);
-  q.num_u = dot(tri.e2, dao);
-  q.num_v = dot(tri.e1, dao);
+  q.num_u = dot(mk(C.x, C.y, C.z), dao);
+  q.num_v = dot(mk(B.x, B.y, B.z), dao);
   q.det = -dn;
-  const float tiny = q.det * kTiny;
-  const bool reject = (q.num_t < q.det * kTMin) | (q.num_u < -tiny) | (q.num_v > tiny) |
-                      ((q.num_u - q.num_v) > q.det * kOnePlus) | (q.num_t > best_k * q.det);
-  q.cand = (dn < 0.0f) & (q.num_t > 0.0f) & (!reject | (q.det < kTiny));
+  q.cand = (dn < 0.0f) & (q.num_t > 0.0f) & !pre_reject(q, best_k);
   if (__builtin_expect(__any(q.cand), 0)) {
     if (q.cand) tri_exact(q, i, m, c, best_k);
   }
 }
 
+// Triangle sources for the brute-force scan: the std430 buffer (wave-uniform -> SGPRs) or the LDS
+// image (3 float4 per triangle = (a.xyz, n.x) (n.yz, e1.xy) (e1.z, e2.xyz)).
+struct GlobalTris {
+  const float4* __restrict__ t;
+  __device__ __forceinline__ void operator()(uint32_t i, float4& A, float4& B, float4& C, float4& N) const {
+    A = t[4 * i];
+    B = t[4 * i + 1];
+    C = t[4 * i + 2];
+    N = t[4 * i + 3];
+  }
+};
+struct LdsTris {
+  const float4* t;
+  __device__ __forceinline__ void operator()(uint32_t i, float4& A, float4& B, float4& C, float4& N) const {
+    const float4 p = t[3 * i], q = t[3 * i + 1], r = t[3 * i + 2];
+    A = make_float4(p.x, p.y, p.z, 0.0f);
+    B = make_float4(q.z, q.w, r.x, 0.0f);
+    C = make_float4(r.y, r.z, r.w, 0.0f);
+    N = make_float4(p.w, q.x, q.y, 0.0f);
+  }
+};
+
+// world_hit (raytracing.glsl:267-288) for one lane: spheres, then every triangle of every mesh whose
+// (quirky) AABB test passes, two-stage exact test, one running closest hit (ties: first in order).
 template <class Src>
-__device__ __forceinline__ Closest world_hit_two_stage(const Scene& sc, const Src& src, const hrt_push_constants& pc,
-                                                       f3 o, f3 d, uint32_t& tests) {
-  Closest c{kFltMax, 0, 0u, 0u};
-  for (int i = 0; i < pc.num_spheres; ++i) {
-    const float t = sphere_dist(sc.spheres[i], o, d);
-    if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
-  }
-  float best_k = c.t * kOnePlus;
-  for (int m = 0; m < pc.num_meshes; ++m) {
-    const hrt_mesh& mesh = sc.meshes[m];
-    const bool pass = aabb_pass(mesh, o, d);
-    tests += pass ? mesh.len : 0u;
-    if (!pass) continue;
-    const uint32_t end = mesh.first_index + mesh.len;
-    for (uint32_t i = mesh.first_index; i < end; ++i) tri_two_stage(src, i, (uint32_t)m, o, d, c, best_k);
-  }
-  return c;
-}
-
-// Primary segments (origin = cam_pos for every active lane of the wave): iterate each mesh's
-// camera-facing list only.  A triangle left out has num_t = dot(cam_pos - a, n) <= 0 (or NaN) -- the
-// same value every primary lane would compute -- so no primary lane can accept it.
-template <class Src, class List>
-__device__ __forceinline__ Closest world_hit_primary(const Scene& sc, const Src& src, const List& list,
-                                                     const TraceParams& P, f3 o, f3 d, uint32_t& tests) {
-  const hrt_push_constants& pc = P.pc;
-  Closest c{kFltMax, 0, 0u, 0u};
-  for (int i = 0; i < pc.num_spheres; ++i) {
-    const float t = sphere_dist(sc.spheres[i], o, d);
-    if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
-  }
-  float best_k = c.t * kOnePlus;
-  for (int m = 0; m < pc.num_meshes; ++m) {
-    const hrt_mesh& mesh = sc.meshes[m];
-    const bool pass = aabb_pass(mesh, o, d);
-    tests += pass ? mesh.len : 0u;
-    if (!pass) continue;
-    const uint32_t k0 = P.cam_start[m], k1 = k0 + P.cam_count[m];
-    for (uint32_t k = k0; k < k1; ++k) {
-      const uint32_t i = list(k);
-      const TriPre q = tri_pre(src(i), o, d, best_k);
-      if (__builtin_expect(__any(q.cand), 0)) {
-        if (q.cand) tri_exact(q, i, (uint32_t)m, c, best_k);
-      }
-    }
-  }
-  return c;
-}
-
-// Primary segments over the compacted camera-facing records (sequential wave-uniform loads, the
-// original triangle index travels in a.w).
-__device__ __forceinline__ Closest world_hit_primary_compact(const Scene& sc, const TraceParams& P, f3 o, f3 d,
-                                                             uint32_t& tests) {
-  const hrt_push_constants& pc = P.pc;
-  Closest c{kFltMax, 0, 0u, 0u};
-  for (int i = 0; i < pc.num_spheres; ++i) {
-    const float t = sphere_dist(sc.spheres[i], o, d);
-    if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
-  }
-  float best_k = c.t * kOnePlus;
-  const float4* __restrict__ ct = P.cam_tris;
-  for (int m = 0; m < pc.num_meshes; ++m) {
-    const hrt_mesh& mesh = sc.meshes[m];
-    const bool pass = aabb_pass(mesh, o, d);
-    tests += pass ? mesh.len : 0u;
-    if (!pass) continue;
-    const uint32_t k0 = P.cam_start[m], k1 = k0 + P.cam_count[m];
-    for (uint32_t k = k0; k < k1; ++k) {
-      const float4 A = ct[4 * k], B = ct[4 * k + 1], C = ct[4 * k + 2], N = ct[4 * k + 3];
-      const TriData td{mk(A.x, A.y, A.z), mk(B.x, B.y, B.z), mk(C.x, C.y, C.z), mk(N.x, N.y, N.z)};
-      const TriPre q = tri_pre(td, o, d, best_k);
-      if (__builtin_expect(__any(q.cand), 0)) {
-        if (q.cand) tri_exact(q, __builtin_bit_cast(uint32_t, A.w), (uint32_t)m, c, best_k);
-      }
-    }
-  }
-  return c;
-}
-
-struct CompactTag {
-  __device__ __forceinline__ uint32_t operator()(uint32_t) const { return 0u; }
-};
-struct CompactAoTag {
-  __device__ __forceinline__ uint32_t operator()(uint32_t) const { return 0u; }
-};
-
-// Primary segments over compacted records carrying the precomputed ao = cam_pos - a and num_t
-// (wave-uniform for primary rays).  Stage A: dn = dot(d, n); a triangle no lane approaches from its
-// front (dn < 0 fails for every lane) cannot be accepted.  Stage B: the rest of the pre-test.
-__device__ __forceinline__ Closest world_hit_primary_ao(const Scene& sc, const TraceParams& P, f3 o, f3 d,
-                                                        uint32_t& tests) {
-  const hrt_push_constants& pc = P.pc;
-  Closest c{kFltMax, 0, 0u, 0u};
-  for (int i = 0; i < pc.num_spheres; ++i) {
-    const float t = sphere_dist(sc.spheres[i], o, d);
-    if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
-  }
-  float best_k = c.t * kOnePlus;
-  const float4* __restrict__ ct = P.cam_tris;
-  for (int m = 0; m < pc.num_meshes; ++m) {
-    const hrt_mesh& mesh = sc.meshes[m];
-    const bool pass = aabb_pass(mesh, o, d);
-    tests += pass ? mesh.len : 0u;
-    if (!pass) continue;
-    const uint32_t k0 = P.cam_start[m], k1 = k0 + P.cam_count[m];
-    for (uint32_t k = k0; k < k1; ++k) {
-      const float4 N = ct[4 * k + 3];
-      const f3 n = mk(N.x, N.y, N.z);
-      const float dn = dot(d, n);
-      if (!__any(dn < 0.0f)) continue;
-      const float4 A = ct[4 * k], B = ct[4 * k + 1], C = ct[4 * k + 2];
-      const f3 ao = mk(A.x, A.y, A.z);
-      TriPre q;
-      q.num_t = A.w;
-      const f3 dao = cross(ao, d);
-      q.num_u = dot(mk(C.x, C.y, C.z), dao);
-      q.num_v = dot(mk(B.x, B.y, B.z), dao);
-      q.det = -dn;
-      const float tiny = q.det * kTiny;
-      const bool reject = (q.num_t < q.det * kTMin) | (q.num_u < -tiny) | (q.num_v > tiny) |
-                          ((q.num_u - q.num_v) > q.det * kOnePlus) | (q.num_t > best_k * q.det);
-      q.cand = (dn < 0.0f) & (!reject | (q.det < kTiny));
-      if (__builtin_expect(__any(q.cand), 0)) {
-        if (q.cand) tri_exact(q, __builtin_bit_cast(uint32_t, B.w), (uint32_t)m, c, best_k);
-      }
-    }
-  }
-  return c;
-}
-
-// Batched form of world_hit_primary_ao: the stage-A loads (normals) of 4 consecutive compacted
-// records are issued together so their latency overlaps; each triangle then branches into stage B
-// on its own wave vote.  Rec is an accessor for the compacted records (global or LDS).
-template <class Rec>
-__device__ __forceinline__ void primary_stage_b(const Rec& rec, uint32_t k, float dn, f3 d, uint32_t m, Closest& c,
-                                                float& best_k) {
-  const float4 A = rec(4 * k), B = rec(4 * k + 1), C = rec(4 * k + 2);
-  const f3 ao = mk(A.x, A.y, A.z);
-  TriPre q;
-  q.num_t = A.w;
-  const f3 dao = cross(ao, d);
-  q.num_u = dot(mk(C.x, C.y, C.z), dao);
-  q.num_v = dot(mk(B.x, B.y, B.z), dao);
-  q.det = -dn;
-  const float tiny = q.det * kTiny;
-  const bool reject = (q.num_t < q.det * kTMin) | (q.num_u < -tiny) | (q.num_v > tiny) |
-                      ((q.num_u - q.num_v) > q.det * kOnePlus) | (q.num_t > best_k * q.det);
-  q.cand = (dn < 0.0f) & (!reject | (q.det < kTiny));
-  if (__builtin_expect(__any(q.cand), 0)) {
-    if (q.cand) tri_exact(q, __builtin_bit_cast(uint32_t, B.w), m, c, best_k);
-  }
-}
-
-template <class Rec>
-__device__ __forceinline__ Closest world_hit_primary_batch(const Scene& sc, const Rec& rec, const TraceParams& P,
-                                                           f3 o, f3 d, uint32_t& tests) {
-  const hrt_push_constants& pc = P.pc;
-  Closest c{kFltMax, 0, 0u, 0u};
-  for (int i = 0; i < pc.num_spheres; ++i) {
-    const float t = sphere_dist(sc.spheres[i], o, d);
-    if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
-  }
-  float best_k = c.t * kOnePlus;
-  for (int m = 0; m < pc.num_meshes; ++m) {
-    const hrt_mesh& mesh = sc.meshes[m];
-    const bool pass = aabb_pass(mesh, o, d);
-    tests += pass ? mesh.len : 0u;
-    if (!pass) continue;
-    const uint32_t k0 = P.cam_start[m], k1 = k0 + P.cam_count[m];
-    uint32_t k = k0;
-    for (; k + 4 <= k1; k += 4) {
-      const float4 N0 = rec(4 * k + 3), N1 = rec(4 * k + 7), N2 = rec(4 * k + 11), N3 = rec(4 * k + 15);
-      const float dn0 = dot(d, mk(N0.x, N0.y, N0.z)), dn1 = dot(d, mk(N1.x, N1.y, N1.z));
-      const float dn2 = dot(d, mk(N2.x, N2.y, N2.z)), dn3 = dot(d, mk(N3.x, N3.y, N3.z));
-      if (__any(dn0 < 0.0f)) primary_stage_b(rec, k, dn0, d, (uint32_t)m, c, best_k);
-      if (__any(dn1 < 0.0f)) primary_stage_b(rec, k + 1, dn1, d, (uint32_t)m, c, best_k);
-      if (__any(dn2 < 0.0f)) primary_stage_b(rec, k + 2, dn2, d, (uint32_t)m, c, best_k);
-      if (__any(dn3 < 0.0f)) primary_stage_b(rec, k + 3, dn3, d, (uint32_t)m, c, best_k);
-    }
-    for (; k < k1; ++k) {
-      const float4 N = rec(4 * k + 3);
-      const float dn = dot(d, mk(N.x, N.y, N.z));
-      if (__any(dn < 0.0f)) primary_stage_b(rec, k, dn, d, (uint32_t)m, c, best_k);
-    }
-  }
-  return c;
-}
-
-struct GlobalRec {
-  const float4* __restrict__ r;
-  __device__ __forceinline__ float4 operator()(uint32_t j) const { return r[j]; }
-};
-struct LdsRec {
-  const float4* r;
-  __device__ __forceinline__ float4 operator()(uint32_t j) const { return r[j]; }
-};
-struct BatchGlobalTag {
-  __device__ __forceinline__ uint32_t operator()(uint32_t) const { return 0u; }
-};
-struct BatchLdsTag {
-  const float4* r;
-  __device__ __forceinline__ uint32_t operator()(uint32_t) const { return 0u; }
-};
-
-struct GlobalList {
-  const uint32_t* __restrict__ l;
-  __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return l[k]; }
-};
-struct LdsList {
-  const uint32_t* l;
-  __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return l[k]; }
-};
-
-template <int G, class Src>
-__device__ __forceinline__ Closest world_hit_tuned(const Scene& sc, const Src& src, const hrt_push_constants& pc,
-                                                   f3 o, f3 d, uint32_t& tests) {
+__device__ __forceinline__ Closest world_hit_brute(const Scene& sc, const Src& src, const hrt_push_constants& pc, f3 o,
+                                                   f3 d, uint32_t& tests) {
   Closest c{kFltMax, 0, 0u, 0u};
   for (int i = 0; i < pc.num_spheres; ++i) {
     const float t = sphere_dist(sc.spheres[i], o, d);
@@ -627,29 +373,20 @@ __device__ __forceinline__ Closest world_hit_tuned(const Scene& sc, const Src& s
     tests += pass ? mesh.len : 0u;
     if (!pass) continue;
     const uint32_t end = mesh.first_index + mesh.len;
-    uint32_t i = mesh.first_index;
-    for (; i + G <= end; i += G) tri_group<G, Src>(src, i, (uint32_t)m, o, d, c, best_k);
-    if (G > 1)
-      for (; i < end; ++i) tri_group<1, Src>(src, i, (uint32_t)m, o, d, c, best_k);
+    for (uint32_t i = mesh.first_index; i < end; ++i) {
+      float4 A, B, C, N;
+      src(i, A, B, C, N);
+      tri_two_stage(A, B, C, N, i, (uint32_t)m, o, d, c, best_k);
+    }
   }
   return c;
 }
 
-// Fused sample/bounce loop: each lane runs its pixel's num_samples paths back to back
-// (RNG state chains through them exactly as raytracing.glsl:379-385); the wave iterates until
-// every lane's last path has ended.
-struct NoList {
-  __device__ __forceinline__ uint32_t operator()(uint32_t) const { return 0u; }
-};
-
-template <int G, class Src, bool TwoStage = false, class List = NoList>
-__device__ __forceinline__ void trace_fused(const TraceParams& P, const Src& src, uint32_t x, uint32_t lr,
-                                            const List& list = List()) {
-  constexpr bool kCamList = !__is_same(List, NoList);
-  constexpr bool kCompact = __is_same(List, CompactTag);
-  constexpr bool kCompactAo = __is_same(List, CompactAoTag);
-  constexpr bool kBatchG = __is_same(List, BatchGlobalTag);
-  constexpr bool kBatchL = __is_same(List, BatchLdsTag);
+// ---- BRUTE / BRUTE_LDS: fused sample/bounce loop ---------------------------------------------------
+// Each lane runs its pixel's num_samples paths back to back (RNG state chains through them exactly
+// as raytracing.glsl:379-385); the wave iterates until every lane's last path has ended.
+template <class Src>
+__device__ __forceinline__ void trace_fused(const TraceParams& P, const Src& src, uint32_t x, uint32_t lr) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
   const uint32_t y = global_row(lr, P);
@@ -672,27 +409,7 @@ __device__ __forceinline__ void trace_fused(const TraceParams& P, const Src& src
         const f3 dir = get_ray_dir(pc, centre, state);
         p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, normalize(dir), 0, true};
       }
-      Closest c;
-      if constexpr (kBatchG) {
-        if (__all(p.bounce == 0))
-          c = world_hit_primary_batch(sc, GlobalRec{P.cam_tris}, P, p.pos, p.dir, tests);
-        else
-          c = world_hit_two_stage(sc, src, pc, p.pos, p.dir, tests);
-      } else if constexpr (kBatchL) {
-        if (__all(p.bounce == 0))
-          c = world_hit_primary_batch(sc, LdsRec{list.r}, P, p.pos, p.dir, tests);
-        else
-          c = world_hit_two_stage(sc, src, pc, p.pos, p.dir, tests);
-      } else if (kCompactAo && __all(p.bounce == 0))
-        c = world_hit_primary_ao(sc, P, p.pos, p.dir, tests);
-      else if (kCompact && __all(p.bounce == 0))
-        c = world_hit_primary_compact(sc, P, p.pos, p.dir, tests);
-      else if (kCamList && !kCompact && !kCompactAo && !kBatchG && !kBatchL && __all(p.bounce == 0))
-        c = world_hit_primary(sc, src, list, P, p.pos, p.dir, tests);
-      else if (TwoStage)
-        c = world_hit_two_stage(sc, src, pc, p.pos, p.dir, tests);
-      else
-        c = world_hit_tuned<G>(sc, src, pc, p.pos, p.dir, tests);
+      const Closest c = world_hit_brute(sc, src, pc, p.pos, p.dir, tests);
       ++segs;
       const bool ended = shade_step(sc, pc, p, c, state);
       ++p.bounce;
@@ -707,29 +424,18 @@ __device__ __forceinline__ void trace_fused(const TraceParams& P, const Src& src
   flush_counters(P, segs, tests);
 }
 
-template <int G>
-__global__ __launch_bounds__(256) void trace_tuned(TraceParams P) {
+__global__ __launch_bounds__(256) void trace_brute(TraceParams P) {
   uint32_t x, lr;
   lane_pixel(P, x, lr);
-  trace_fused<G>(P, GlobalTris{P.tris}, x, lr);
+  trace_fused(P, GlobalTris{reinterpret_cast<const float4*>(P.tris)}, x, lr);
 }
 
-__global__ __launch_bounds__(256) void trace_tuned_f4(TraceParams P) {
-  uint32_t x, lr;
-  lane_pixel(P, x, lr);
-  trace_fused<1>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr);
-}
-
-// Whole scene resident in LDS (3 float4 per triangle), 1024-thread workgroups (16 waves, a 32x32
-// pixel tile of 8x8 wave tiles): the copy is paid once per workgroup, every wave then streams the
-// triangles from LDS with broadcast reads instead of scalar loads.
+// Whole scene resident in LDS, 1024-thread workgroups (16 waves, a 32x32 pixel tile of 8x8 wave
+// tiles): the copy is paid once per workgroup, every wave then streams the triangles from LDS with
+// broadcast reads instead of scalar loads.
 extern __shared__ float4 lds_tris[];
-template <bool TwoStage, bool CamList = false>
-__global__ __launch_bounds__(1024) void trace_lds(TraceParams P) {
+__global__ __launch_bounds__(1024) void trace_brute_lds(TraceParams P) {
   const uint32_t n = P.n_tris;
-  uint32_t* lds_list = reinterpret_cast<uint32_t*>(lds_tris + 3 * n);
-  if (CamList)
-    for (uint32_t k = threadIdx.x; k < P.cam_list_capacity; k += blockDim.x) lds_list[k] = P.cam_list[k];
   for (uint32_t k = threadIdx.x; k < 3 * n; k += blockDim.x) {
     const uint32_t i = k / 3, part = k - 3 * i;
     const hrt_triangle& t = P.tris[i];
@@ -743,65 +449,28 @@ __global__ __launch_bounds__(1024) void trace_lds(TraceParams P) {
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t x = blockIdx.x * 32 + (wave & 3) * 8 + (lane & 7);
   const uint32_t lr = blockIdx.y * 32 + (wave >> 2) * 8 + (lane >> 3);
-  if (CamList)
-    trace_fused<1, LdsTris, TwoStage, LdsList>(P, LdsTris{lds_tris}, x, lr, LdsList{lds_list});
-  else
-    trace_fused<1, LdsTris, TwoStage>(P, LdsTris{lds_tris}, x, lr);
+  trace_fused(P, LdsTris{lds_tris}, x, lr);
 }
 
-__global__ __launch_bounds__(256) void trace_camlist_f4(TraceParams P) {
-  uint32_t x, lr;
-  lane_pixel(P, x, lr);
-  trace_fused<1, GlobalTris4, true, GlobalList>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr,
-                                                GlobalList{P.cam_list});
-}
-
-__global__ __launch_bounds__(256) void trace_camcompact_f4(TraceParams P) {
-  uint32_t x, lr;
-  lane_pixel(P, x, lr);
-  trace_fused<1, GlobalTris4, true, CompactTag>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr,
-                                                CompactTag{});
-}
-
-__global__ __launch_bounds__(256) void trace_camao_f4(TraceParams P) {
-  uint32_t x, lr;
-  lane_pixel(P, x, lr);
-  trace_fused<1, GlobalTris4, true, CompactAoTag>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr,
-                                                  CompactAoTag{});
-}
-
-__global__ __launch_bounds__(256) void trace_batch_f4(TraceParams P) {
-  uint32_t x, lr;
-  lane_pixel(P, x, lr);
-  trace_fused<1, GlobalTris4, true, BatchGlobalTag>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr,
-                                                    BatchGlobalTag{});
-}
-
-// Compacted camera-facing records resident in LDS (64 B each), the generic path on scalar loads.
-__global__ __launch_bounds__(1024) void trace_batch_lds(TraceParams P) {
-  const uint32_t nrec = 4 * P.cam_list_capacity;
-  for (uint32_t k = threadIdx.x; k < nrec; k += blockDim.x) lds_tris[k] = P.cam_tris[k];
-  __syncthreads();
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t x = blockIdx.x * 32 + (wave & 3) * 8 + (lane & 7);
-  const uint32_t lr = blockIdx.y * 32 + (wave >> 2) * 8 + (lane >> 3);
-  trace_fused<1, GlobalTris4, true, BatchLdsTag>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr,
-                                                 BatchLdsTag{lds_tris});
-}
-
-// ---- variant 14: primary-ray bundle culling -------------------------------------------------------
+// ---- BUNDLE / BUNDLE_CULL ------------------------------------------------------------------------
 //
-// For a primary segment every lane's ray starts at cam_pos, so for a fixed triangle the reference's
-// det = -d.n, num_u = d.(e2 x ao) and num_v = d.(e1 x ao) are LINEAR in the lane's direction d
-// (ao = cam_pos - a is shared).  Bounding d over the wave's directions (axis a, cos range [c_lo,c_hi],
-// sine bound s_hi) bounds each linear form; a triangle is rejected for the whole wave when
+// Per-frame prep (camera_lists): for every mesh, the triangles with num_t = dot(cam_pos - a, n) > 0
+// -- computed exactly as a primary lane computes it -- compacted in buffer order into records
+// (ao, num_t) (e1, index) (e2, -) (n, -), plus 5 float4 bundle-cull records (g, margin) per triangle.
+// A triangle left out cannot be accepted by any primary lane (its dist would be <= 0 or NaN).
+//
+// Bundle cull: for a primary segment every lane's ray starts at cam_pos, so for a fixed triangle the
+// reference's det = -d.n, num_u = d.(e2 x ao) and num_v = d.(e1 x ao) are LINEAR in the lane's
+// direction d (ao = cam_pos - a is shared).  Bounding d over the wave's directions (axis a, cosine
+// range [c_lo, c_hi], sine bound s_hi) bounds each linear form; a triangle is rejected for the whole
+// wave when
 //   R1  min d.n            > m_n   (every lane: dn >= 0, raytracing.glsl:217)
 //   R3  max d.(e2 x ao)    < -m_u  (every lane: u < 0)
 //   R4  min d.(e1 x ao)    > m_v   (every lane: v < 0)
 //   R5  min d.(g_u-h+n)    > m_w   (every lane: num_u - num_v > det(1+2^-16), so u, v or w < 0)
 // with margins m_* = 1e-5 * (product norms) + 2^-40|n| (+2^-14|n| for R5) covering the rounding of the
 // reference's own dot/cross sequence (<= ~10 eps * product norm) and of these bounds.  The cull runs
-// lane-parallel: lane j bounds triangle base+j, so 64 triangles cost one pass.  Survivors (in buffer
+// lane-parallel: lane j bounds triangle base+j, so 64 triangles cost one pass; survivors (in buffer
 // order) get the exact per-lane test.
 struct Bundle {
   f3 a;
@@ -813,6 +482,23 @@ __device__ __forceinline__ float wave_min_all(float v) {  // all 64 lanes active
   for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
   return v;
 }
+__device__ __forceinline__ float wave_max_all(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Direction cone of the lanes with sel == true (axis = the first such lane's direction).
+__device__ __forceinline__ Bundle make_bundle(bool sel, f3 d) {
+  const int lead = __builtin_ctzll(__ballot(sel));
+  Bundle b;
+  b.a = mk(__shfl(d.x, lead, 64), __shfl(d.y, lead, 64), __shfl(d.z, lead, 64));
+  const float lam = sel ? dot(d, b.a) : 3.0f;
+  b.c_lo = wave_min_all(lam) - 1e-5f;
+  b.c_hi = 1.00001f;
+  b.s_hi = (b.c_lo > 0.0f) ? __builtin_sqrtf(fmaxf(0.0f, 1.00002f - b.c_lo * b.c_lo)) * 1.00001f + 1e-6f : 1.00001f;
+  return b;
+}
 
 __device__ __forceinline__ float lin_lower(float ga, float gn, const Bundle& b) {
   return fminf(b.c_lo * ga, b.c_hi * ga) - b.s_hi * gn;
@@ -821,25 +507,40 @@ __device__ __forceinline__ float lin_upper(float ga, float gn, const Bundle& b) 
   return fmaxf(b.c_lo * ga, b.c_hi * ga) + b.s_hi * gn;
 }
 
+// Spheres for the selected lanes (raytracing.glsl:271-276).
+__device__ __forceinline__ void spheres_first(const Scene& sc, const hrt_push_constants& pc, bool sel, f3 o, f3 d,
+                                              Closest& c) {
+  if (!sel) return;
+  c = Closest{kFltMax, 0, 0u, 0u};
+  for (int i = 0; i < pc.num_spheres; ++i) {
+    const float t = sphere_dist(sc.spheres[i], o, d);
+    if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
+  }
+}
+
+// Exact per-lane test of compacted camera-facing record k (ao and num_t precomputed), entered only
+// when some lane has dn < 0.
+__device__ __forceinline__ void primary_exact(const float4* __restrict__ ct, uint32_t k, float dn, f3 d, uint32_t m,
+                                              Closest& c, float& best_k) {
+  const float4 A = ct[4 * k], B = ct[4 * k + 1], C = ct[4 * k + 2];
+  TriPre q;
+  q.num_t = A.w;
+  const f3 dao = cross(mk(A.x, A.y, A.z), d);
+  q.num_u = dot(mk(C.x, C.y, C.z), dao);
+  q.num_v = dot(mk(B.x, B.y, B.z), dao);
+  q.det = -dn;
+  q.cand = (dn < 0.0f) & !pre_reject(q, best_k);
+  if (__builtin_expect(__any(q.cand), 0)) {
+    if (q.cand) tri_exact(q, __builtin_bit_cast(uint32_t, B.w), m, c, best_k);
+  }
+}
+
 // Primary segments of the lanes with prim == true.  Called with ALL 64 lanes of the wave active.
 __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TraceParams& P, bool prim, f3 o, f3 d,
                                                  uint32_t& tests, Closest& c) {
   const hrt_push_constants& pc = P.pc;
-  const unsigned long long pm = __ballot(prim);
-  const int lead = __builtin_ctzll(pm);
-  Bundle b;
-  b.a = mk(__shfl(d.x, lead, 64), __shfl(d.y, lead, 64), __shfl(d.z, lead, 64));
-  const float lam = prim ? dot(d, b.a) : 3.0f;
-  b.c_lo = wave_min_all(lam) - 1e-5f;
-  b.c_hi = 1.00001f;
-  b.s_hi = (b.c_lo > 0.0f) ? __builtin_sqrtf(fmaxf(0.0f, 1.00002f - b.c_lo * b.c_lo)) * 1.00001f + 1e-6f : 1.00001f;
-  if (prim) {
-    c = Closest{kFltMax, 0, 0u, 0u};
-    for (int i = 0; i < pc.num_spheres; ++i) {
-      const float t = sphere_dist(sc.spheres[i], o, d);
-      if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
-    }
-  }
+  const Bundle b = make_bundle(prim, d);
+  spheres_first(sc, pc, prim, o, d, c);
   float best_k = c.t * kOnePlus;
   const float4* __restrict__ ct = P.cam_tris;
   const float4* __restrict__ cr = P.cam_cull;
@@ -863,73 +564,83 @@ __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TracePar
       }
       unsigned long long mask = __ballot(keep);
       while (mask) {
-        const uint32_t j = __builtin_ctzll(mask);
+        const uint32_t kk = base + (uint32_t)__builtin_ctzll(mask);
         mask &= mask - 1ull;
-        const uint32_t kk = base + j;
         if (pass) {
           const float4 N = ct[4 * kk + 3];
           const float dn = dot(d, mk(N.x, N.y, N.z));
-          if (__any(dn < 0.0f)) primary_stage_b(GlobalRec{ct}, kk, dn, d, (uint32_t)m, c, best_k);
+          if (__any(dn < 0.0f)) primary_exact(ct, kk, dn, d, (uint32_t)m, c, best_k);
         }
       }
     }
   }
 }
 
-// Bounce-path world_hit with the next triangle's 64-byte record loaded (wave-uniform, into SGPRs)
-// while the current one is tested: the loop no longer waits a full scalar-load latency per triangle.
-__device__ __forceinline__ void tri_two_stage_rec(const float4& A, const float4& B, const float4& C, const float4& N,
-                                                  uint32_t i, uint32_t m, f3 o, f3 d, Closest& c, float& best_k) {
-  const f3 n = mk(N.x, N.y, N.z);
-  const f3 ao = o - mk(A.x, A.y, A.z);
-  TriPre q;
-  q.num_t = dot(ao, n);
-  if (!__any(q.num_t > 0.0f)) return;
-  const float dn = dot(d, n);
-  const f3 dao = cross(ao, d);
-  q.num_u = dot(mk(C.x, C.y, C.z), dao);
-  q.num_v = dot(mk(B.x, B.y, B.z), dao);
-  q.det = -dn;
-  const float tiny = q.det * kTiny;
-  const bool reject = (q.num_t < q.det * kTMin) | (q.num_u < -tiny) | (q.num_v > tiny) |
-                      ((q.num_u - q.num_v) > q.det * kOnePlus) | (q.num_t > best_k * q.det);
-  q.cand = (dn < 0.0f) & (q.num_t > 0.0f) & (!reject | (q.det < kTiny));
-  if (__builtin_expect(__any(q.cand), 0)) {
-    if (q.cand) tri_exact(q, i, m, c, best_k);
-  }
-}
-
-__device__ __forceinline__ Closest world_hit_prefetch(const Scene& sc, const hrt_push_constants& pc, f3 o, f3 d,
-                                                      uint32_t& tests) {
-  Closest c{kFltMax, 0, 0u, 0u};
-  for (int i = 0; i < pc.num_spheres; ++i) {
-    const float t = sphere_dist(sc.spheres[i], o, d);
-    if (t > 0.001f && t < c.t) c = Closest{t, 1, (uint32_t)i, 0u};
-  }
+// Bounce segments with a lane-parallel pre-cull (BUNDLE_CULL).  For the bounce lanes (origins o_l,
+// directions d_l) and triangle (a, n):
+//   S1  num_t = (o - a).n is linear in o: if max over the lanes' origin box B of (o - a).n
+//       < -1e-5 |o - a|max |n|_1, every lane computes num_t <= 0 -> dist <= 0 (or NaN): rejected;
+//   R1  dn = d.n is linear in d: if min over the lanes' direction cone of d.n > 1e-5 |n|_1, every
+//       lane has dn >= 0: rejected.
+// Lane j bounds triangle base+j; survivors (buffer order) get the exact per-lane two-stage test.
+// Called with ALL 64 lanes active.
+__device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const TraceParams& P, bool sec, f3 o, f3 d,
+                                                      uint32_t& tests, Closest& c) {
+  const hrt_push_constants& pc = P.pc;
+  const float inf = __builtin_inff();
+  const f3 lo = mk(wave_min_all(sec ? o.x : inf), wave_min_all(sec ? o.y : inf), wave_min_all(sec ? o.z : inf));
+  const f3 hi = mk(wave_max_all(sec ? o.x : -inf), wave_max_all(sec ? o.y : -inf), wave_max_all(sec ? o.z : -inf));
+  const Bundle b = make_bundle(sec, d);
+  const bool box_ok = (hi.x - lo.x) <= 3.0e38f && (hi.y - lo.y) <= 3.0e38f && (hi.z - lo.z) <= 3.0e38f;
+  const f3 ctr = mk(0.5f * lo.x + 0.5f * hi.x, 0.5f * lo.y + 0.5f * hi.y, 0.5f * lo.z + 0.5f * hi.z);
+  // half widths, enlarged so that |o - ctr| <= hw per axis for every bounce lane despite rounding
+  const f3 hw = mk((hi.x - ctr.x) * 1.0001f, (hi.y - ctr.y) * 1.0001f, (hi.z - ctr.z) * 1.0001f);
+  spheres_first(sc, pc, sec, o, d, c);
   float best_k = c.t * kOnePlus;
   const float4* __restrict__ T = reinterpret_cast<const float4*>(sc.tris);
+  const uint32_t lane = threadIdx.x & 63;
   for (int m = 0; m < pc.num_meshes; ++m) {
     const hrt_mesh& mesh = sc.meshes[m];
-    const bool pass = aabb_pass(mesh, o, d);
-    tests += pass ? mesh.len : 0u;
-    if (!pass) continue;
-    const uint32_t first = mesh.first_index, end = first + mesh.len;
-    if (first >= end) continue;
-    float4 A = T[4 * first], B = T[4 * first + 1], C = T[4 * first + 2], N = T[4 * first + 3];
-    for (uint32_t i = first; i < end; ++i) {
-      const uint32_t nx = (i + 1 < end) ? i + 1 : i;  // in-bounds prefetch of the next record
-      const float4 A1 = T[4 * nx], B1 = T[4 * nx + 1], C1 = T[4 * nx + 2], N1 = T[4 * nx + 3];
-      tri_two_stage_rec(A, B, C, N, i, (uint32_t)m, o, d, c, best_k);
-      A = A1; B = B1; C = C1; N = N1;
+    const bool pass = sec && aabb_pass(mesh, o, d);
+    if (sec) tests += pass ? mesh.len : 0u;
+    if (!__any(pass)) continue;
+    const uint32_t k0 = mesh.first_index, k1 = k0 + mesh.len;
+    for (uint32_t base = k0; base < k1; base += 64) {
+      const uint32_t k = base + lane;
+      bool keep = false;
+      if (k < k1) {
+        const float4 A = T[4 * k], N = T[4 * k + 3];
+        const f3 n = mk(N.x, N.y, N.z);
+        const f3 ca = ctr - mk(A.x, A.y, A.z);
+        const float an = fabsf(n.x), bn = fabsf(n.y), cn = fabsf(n.z);
+        const float nn = an + bn + cn;                                                      // >= |n|
+        const float spread = an * hw.x + bn * hw.y + cn * hw.z;                             // max (o - ctr).n
+        const float reach = fabsf(ca.x) + fabsf(ca.y) + fabsf(ca.z) + hw.x + hw.y + hw.z;  // >= |o - a|
+        const bool s1 = box_ok && (dot(ca, n) + spread + 1e-5f * reach * nn < 0.0f);
+        const bool r1 = lin_lower(dot(n, b.a), nn, b) > 1e-5f * nn;
+        keep = !(s1 | r1);
+      }
+      unsigned long long mask = __ballot(keep);
+      while (mask) {
+        const uint32_t kk = base + (uint32_t)__builtin_ctzll(mask);
+        mask &= mask - 1ull;
+        if (pass) tri_two_stage(T[4 * kk], T[4 * kk + 1], T[4 * kk + 2], T[4 * kk + 3], kk, (uint32_t)m, o, d, c,
+                                best_k);
+      }
     }
   }
-  return c;
 }
 
-template <class Src, bool Prefetch = false>
-__device__ __forceinline__ void trace_fused_split(const TraceParams& P, const Src& src, uint32_t x, uint32_t lr) {
+// Fused loop of BUNDLE / BUNDLE_CULL.  Every lane stays in the loop until the whole wave is done, so
+// the loop top is a full-wave region (lane-parallel culls and shuffles need all 64 lanes).  Primary
+// segments take the bundle path; a lane whose next segment is a bounce waits (state untouched) until
+// at least sec_batch lanes wait or no primary segment is left in the wave, then all waiting lanes run
+// their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
+template <bool BounceCull>
+__device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
+  const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
   const uint32_t y = global_row(lr, P);
   uint32_t segs = 0, tests = 0;
   const bool active = x < pc.width && lr < P.local_rows && y < pc.height;
@@ -946,7 +657,6 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, const Sr
   Path p;
   p.bounce = pc.max_bounces + 1;
   bool done = !active;
-  // every lane stays in the loop until the whole wave is done (full-wave region at the loop top)
   while (__any(!done)) {
     if (!done && p.bounce > pc.max_bounces) {
       if (sample >= pc.num_samples) {
@@ -958,22 +668,18 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, const Sr
       }
     }
     const bool prim = !done && p.bounce == 0;
-    const bool sec_ready = !done && p.bounce != 0;
-    // Deferred secondaries: a lane whose next segment is a bounce waits (its state untouched) until
-    // at least sec_batch lanes are waiting or no primary lane is left, so the brute-force bounce
-    // path runs on well-filled waves.  Per-pixel order of work is unchanged.
-    const uint32_t nsec = (uint32_t)__popcll(__ballot(sec_ready));
+    const bool waiting = !done && p.bounce != 0;
+    const uint32_t nwait = (uint32_t)__popcll(__ballot(waiting));
     const bool any_prim = __any(prim);
-    const bool run_sec = nsec > 0 && (nsec >= P.sec_batch || !any_prim);
-    const bool sec = sec_ready && run_sec;
+    const bool run_sec = nwait > 0 && (nwait >= P.sec_batch || !any_prim);
+    const bool sec = waiting && run_sec;
     Closest c{kFltMax, 0, 0u, 0u};
     if (any_prim) world_hit_bundle(sc, P, prim, p.pos, p.dir, tests, c);
     if (run_sec) {
-      if (sec) {
-        if constexpr (Prefetch)
-          c = world_hit_prefetch(sc, pc, p.pos, p.dir, tests);
-        else
-          c = world_hit_two_stage(sc, src, pc, p.pos, p.dir, tests);
+      if constexpr (BounceCull) {
+        world_hit_bounce_cull(sc, P, sec, p.pos, p.dir, tests, c);
+      } else {
+        if (sec) c = world_hit_brute(sc, src, pc, p.pos, p.dir, tests);
       }
     }
     if (prim || sec) {
@@ -996,23 +702,17 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, const Sr
 __global__ __launch_bounds__(256) void trace_bundle(TraceParams P) {
   uint32_t x, lr;
   lane_pixel(P, x, lr);
-  trace_fused_split(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr);
+  trace_fused_split<false>(P, x, lr);
 }
 
-__global__ __launch_bounds__(256) void trace_bundle_pf(TraceParams P) {
+__global__ __launch_bounds__(256) void trace_bundle_cull(TraceParams P) {
   uint32_t x, lr;
   lane_pixel(P, x, lr);
-  trace_fused_split<GlobalTris4, true>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr);
+  trace_fused_split<true>(P, x, lr);
 }
 
-__global__ __launch_bounds__(256, 8) void trace_bundle_pf8(TraceParams P) {
-  uint32_t x, lr;
-  lane_pixel(P, x, lr);
-  trace_fused_split<GlobalTris4, true>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr);
-}
-
-// Per-frame prep for the camera-facing lists: one workgroup per mesh, order-preserving compaction
-// of the mesh's triangles with num_t(cam_pos) > 0, computed exactly as the trace kernel does.
+// Per-frame prep for the bundle variants: one workgroup per mesh, order-preserving compaction of the
+// mesh's camera-facing triangles (num_t(cam_pos) > 0, computed exactly as the trace kernel does).
 __global__ __launch_bounds__(256) void camera_lists(TraceParams P) {
   const uint32_t m = blockIdx.x;
   const hrt_mesh& mesh = P.meshes[m];
@@ -1026,10 +726,13 @@ __global__ __launch_bounds__(256) void camera_lists(TraceParams P) {
   for (uint32_t c0 = 0; c0 < mesh.len; c0 += 256) {
     const uint32_t k = c0 + threadIdx.x;
     bool keep = false;
+    f3 ao = mk(0.0f, 0.0f, 0.0f);
+    float nt = 0.0f;
     if (k < mesh.len) {
       const hrt_triangle& t = P.tris[mesh.first_index + k];
-      const f3 ao = o - ld3(t.a);
-      keep = dot(ao, ld3(t.normal)) > 0.0f;
+      ao = o - ld3(t.a);
+      nt = dot(ao, ld3(t.normal));
+      keep = nt > 0.0f;
     }
     const unsigned long long ballot = __ballot(keep);
     const uint32_t prefix = __popcll(ballot & ((1ull << lane) - 1ull));
@@ -1040,44 +743,25 @@ __global__ __launch_bounds__(256) void camera_lists(TraceParams P) {
     for (uint32_t w = 0; w < wave; ++w) off += wave_counts[w];
     if (keep) {
       const uint32_t dst = start + off + prefix, idx = mesh.first_index + k;
-      P.cam_list[dst] = idx;
-      if (P.cam_tris) {
-        const float4* src = reinterpret_cast<const float4*>(P.tris) + 4 * (size_t)idx;
-        float4* out = P.cam_tris + 4 * (size_t)dst;
-        if (P.cam_layout == 1) {
-          // (ao, num_t) (e1, idx) (e2, -) (n, -): ao and num_t exactly as a primary lane computes them
-          const hrt_triangle& t = P.tris[idx];
-          const f3 ao = o - ld3(t.a);
-          const float nt = dot(ao, ld3(t.normal));
-          out[0] = make_float4(ao.x, ao.y, ao.z, nt);
-          float4 e1 = src[1];
-          e1.w = __builtin_bit_cast(float, idx);
-          out[1] = e1;
-        } else {
-          float4 a = src[0];
-          a.w = __builtin_bit_cast(float, idx);
-          out[0] = a;
-          out[1] = src[1];
-        }
-        out[2] = src[2];
-        out[3] = src[3];
-        if (P.cam_cull) {
-          const hrt_triangle& t = P.tris[idx];
-          const f3 ao = o - ld3(t.a);
-          const f3 n = ld3(t.normal), e1 = ld3(t.edge_one), e2 = ld3(t.edge_two);
-          const f3 gu = cross(e2, ao), h = cross(e1, ao);
-          const f3 kw = (gu - h) + n;
-          auto nrm = [](f3 v) { return __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z) * 1.0001f; };
-          const float pn = nrm(n), pao = nrm(ao), pu = nrm(e2) * pao, pv = nrm(e1) * pao;
-          const float tiny = pn * 9.094947017729282e-13f;  // 2^-40 |n|
-          float4* cc = P.cam_cull + 5 * (size_t)dst;
-          cc[0] = make_float4(n.x, n.y, n.z, 1e-5f * pn);
-          cc[1] = make_float4(gu.x, gu.y, gu.z, 1e-5f * pu + tiny);
-          cc[2] = make_float4(h.x, h.y, h.z, 1e-5f * pv + tiny);
-          cc[3] = make_float4(kw.x, kw.y, kw.z, 1e-5f * (pu + pv + pn) + pn * 6.103515625e-05f);
-          cc[4] = make_float4(pn, fmaxf(nrm(gu), pu), fmaxf(nrm(h), pv), nrm(kw) + 1e-5f * (pu + pv + pn));
-        }
-      }
+      const hrt_triangle& t = P.tris[idx];
+      const f3 n = ld3(t.normal), e1 = ld3(t.edge_one), e2 = ld3(t.edge_two);
+      float4* out = P.cam_tris + 4 * (size_t)dst;
+      out[0] = make_float4(ao.x, ao.y, ao.z, nt);
+      out[1] = make_float4(e1.x, e1.y, e1.z, __builtin_bit_cast(float, idx));
+      out[2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
+      out[3] = make_float4(n.x, n.y, n.z, 0.0f);
+      // bundle-cull record: the linear forms' coefficients and their margins
+      const f3 gu = cross(e2, ao), h = cross(e1, ao);
+      const f3 kw = (gu - h) + n;
+      auto nrm = [](f3 v) { return __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z) * 1.0001f; };
+      const float pn = nrm(n), pao = nrm(ao), pu = nrm(e2) * pao, pv = nrm(e1) * pao;
+      const float tiny = pn * 9.094947017729282e-13f;  // 2^-40 |n|
+      float4* cc = P.cam_cull + 5 * (size_t)dst;
+      cc[0] = make_float4(n.x, n.y, n.z, 1e-5f * pn);
+      cc[1] = make_float4(gu.x, gu.y, gu.z, 1e-5f * pu + tiny);
+      cc[2] = make_float4(h.x, h.y, h.z, 1e-5f * pv + tiny);
+      cc[3] = make_float4(kw.x, kw.y, kw.z, 1e-5f * (pu + pv + pn) + pn * 6.103515625e-05f);
+      cc[4] = make_float4(pn, fmaxf(nrm(gu), pu), fmaxf(nrm(h), pv), nrm(kw) + 1e-5f * (pu + pv + pn));
     }
     __syncthreads();
     if (threadIdx.x == 0) base_s += wave_counts[0] + wave_counts[1] + wave_counts[2] + wave_counts[3];
@@ -1087,12 +771,6 @@ __global__ __launch_bounds__(256) void camera_lists(TraceParams P) {
     P.cam_start[m] = start;
     P.cam_count[m] = base_s;
   }
-}
-
-__global__ __launch_bounds__(256) void trace_two_stage_f4(TraceParams P) {
-  uint32_t x, lr;
-  lane_pixel(P, x, lr);
-  trace_fused<1, GlobalTris4, true>(P, GlobalTris4{reinterpret_cast<const float4*>(P.tris)}, x, lr);
 }
 
 // ---- init clear (raytracing.glsl:363-366) and image_combiner.glsl (:22-43) ----------------------
@@ -1156,67 +834,45 @@ namespace hrt {
 
 static inline unsigned blocks_for(size_t n) { return (unsigned)((n + 255) / 256); }
 constexpr size_t kMaxLdsScene = 160 * 1024;
+constexpr uint32_t kAutoCullTris = 256;  // BUNDLE_CULL from this many mesh triangles, BUNDLE below
+
+int resolve_variant(const TraceParams& p, int variant) {
+  if (variant == HRT_KERNEL_AUTO) variant = p.cam_list_capacity >= kAutoCullTris ? HRT_KERNEL_BUNDLE_CULL
+                                                                                 : HRT_KERNEL_BUNDLE;
+  if (variant == HRT_KERNEL_BRUTE_LDS && (size_t)p.n_tris * 48 > kMaxLdsScene) variant = HRT_KERNEL_BRUTE;
+  if (p.pc.max_bounces < 0) variant = HRT_KERNEL_LITERAL;  // the fused loops assume >= 1 segment per path
+  return variant;
+}
 
 hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream) {
   static bool lds_attr = false;
   if (!lds_attr) {
     lds_attr = true;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_lds<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_lds<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_lds<true, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_batch_lds),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_brute_lds),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
   }
+  variant = resolve_variant(p, variant);
   const dim3 grid((p.pc.width + 15) / 16, (p.local_rows + 15) / 16, 1);
-  const size_t lds_bytes = (size_t)p.n_tris * 48;
-  if (variant == 0) variant = 14;  // auto: primary bundle cull + deferred two-stage bounce path
-  const size_t lds_list_bytes = lds_bytes + (size_t)p.cam_list_capacity * 4;
-  if (variant == 8 && lds_list_bytes > kMaxLdsScene) variant = 9;
-  if ((variant == 5 || variant == 6) && lds_bytes > kMaxLdsScene) variant = (variant == 6) ? 7 : 3;
-  const size_t lds_rec_bytes = (size_t)p.cam_list_capacity * 64;
-  if (variant == 12 && lds_rec_bytes > kMaxLdsScene) variant = 13;
-  if (variant >= 8 && variant <= 16 && p.pc.num_meshes > 0) {
-    TraceParams q = p;
-    if (variant == 8 || variant == 9) q.cam_tris = nullptr;
-    q.cam_layout = (variant >= 11) ? 1u : 0u;
-    if (variant < 14) q.cam_cull = nullptr;
-    camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(q);
-  }
   switch (variant) {
-    case 1: trace_literal<<<grid, 256, 0, stream>>>(p); break;
-    case 3: trace_tuned_f4<<<grid, 256, 0, stream>>>(p); break;
-    case 4: trace_tuned<2><<<grid, 256, 0, stream>>>(p); break;
-    case 5:
-    case 6: {
+    case HRT_KERNEL_LITERAL:
+      trace_literal<<<grid, 256, 0, stream>>>(p);
+      break;
+    case HRT_KERNEL_BRUTE_LDS: {
       const dim3 g32((p.pc.width + 31) / 32, (p.local_rows + 31) / 32, 1);
-      if (variant == 5)
-        trace_lds<false><<<g32, 1024, lds_bytes, stream>>>(p);
+      trace_brute_lds<<<g32, 1024, (size_t)p.n_tris * 48, stream>>>(p);
+      break;
+    }
+    case HRT_KERNEL_BUNDLE:
+    case HRT_KERNEL_BUNDLE_CULL:
+      if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      if (variant == HRT_KERNEL_BUNDLE)
+        trace_bundle<<<grid, 256, 0, stream>>>(p);
       else
-        trace_lds<true><<<g32, 1024, lds_bytes, stream>>>(p);
+        trace_bundle_cull<<<grid, 256, 0, stream>>>(p);
       break;
-    }
-    case 7: trace_two_stage_f4<<<grid, 256, 0, stream>>>(p); break;
-    case 8: {
-      const dim3 g32((p.pc.width + 31) / 32, (p.local_rows + 31) / 32, 1);
-      trace_lds<true, true><<<g32, 1024, lds_list_bytes, stream>>>(p);
+    default:
+      trace_brute<<<grid, 256, 0, stream>>>(p);
       break;
-    }
-    case 9: trace_camlist_f4<<<grid, 256, 0, stream>>>(p); break;
-    case 10: trace_camcompact_f4<<<grid, 256, 0, stream>>>(p); break;
-    case 11: trace_camao_f4<<<grid, 256, 0, stream>>>(p); break;
-    case 12: {
-      const dim3 g32((p.pc.width + 31) / 32, (p.local_rows + 31) / 32, 1);
-      trace_batch_lds<<<g32, 1024, lds_rec_bytes, stream>>>(p);
-      break;
-    }
-    case 13: trace_batch_f4<<<grid, 256, 0, stream>>>(p); break;
-    case 14: trace_bundle<<<grid, 256, 0, stream>>>(p); break;
-    case 15: trace_bundle_pf<<<grid, 256, 0, stream>>>(p); break;
-    case 16: trace_bundle_pf8<<<grid, 256, 0, stream>>>(p); break;
-    default: trace_tuned<1><<<grid, 256, 0, stream>>>(p); break;  // 2
   }
   return hipGetLastError();
 }

@@ -147,9 +147,20 @@ typedef struct hrt_stats {
 
 typedef struct hrt_context hrt_context;
 
+/* Trace kernel variants (HRT_OPT_KERNEL_VARIANT).  All produce byte-identical frames and counters;
+ * they differ only in how much of the reference's brute-force work they prove unnecessary. */
+typedef enum hrt_kernel {
+  HRT_KERNEL_AUTO = 0,        /* BUNDLE_CULL for scenes with >= 256 mesh triangles, BUNDLE below */
+  HRT_KERNEL_LITERAL = 1,     /* raytracing.glsl's loop shape, the full test on every triangle */
+  HRT_KERNEL_BRUTE = 2,       /* fused sample/bounce loop, two-stage exact pre-test, triangles via SGPRs */
+  HRT_KERNEL_BRUTE_LDS = 3,   /* BRUTE with the scene resident in LDS (falls back to BRUTE above 160 KiB) */
+  HRT_KERNEL_BUNDLE = 4,      /* primary rays: lane-parallel bundle cull; bounces: deferred, BRUTE test */
+  HRT_KERNEL_BUNDLE_CULL = 5  /* BUNDLE + lane-parallel origin-box / direction-cone cull of bounce rays */
+} hrt_kernel;
+
 /* Option keys for hrt_set_option. */
 typedef enum hrt_option {
-  /* kernel variant: 0 = tuned (default), 1 = literal per-sample loop (same results, A/B and parity) */
+  /* trace kernel variant (hrt_kernel), default HRT_KERNEL_AUTO */
   HRT_OPT_KERNEL_VARIANT = 1,
   /* 1 = count segments / triangle tests on the device (default 1; 0 removes the counters' cost) */
   HRT_OPT_COUNTERS = 2,

@@ -14,7 +14,7 @@ from helpers import E, SceneCase, _lib, mismatch_report
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [0, 1]  # auto (tuned), literal
-ALL_VARIANTS = list(range(17))  # every kernel variant (hrt_set_option HRT_OPT_KERNEL_VARIANT)
+ALL_VARIANTS = list(range(6))  # every hrt_kernel value  # every kernel variant (hrt_set_option HRT_OPT_KERNEL_VARIANT)
 
 CONFIGS = [
     # (scene, size, spp, bounces, rng_offset)

@@ -21,7 +21,7 @@ from helpers import SceneCase, _lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", type=int, nargs="+", default=[1, 2, 3, 4])
+    ap.add_argument("--variants", type=int, nargs="+", default=[1, 2, 3, 4, 5], help="hrt_kernel values")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--scene", default="island")
     ap.add_argument("--size", default="1920x1080")
@@ -41,7 +41,7 @@ def main():
         ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
         ctx.trace(pc)
         ref = ctx.read(_lib.IMG_TRACE)
-    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v >= 14 else [a.sec_batch[0]])]
+    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v in (0, 4, 5) else [a.sec_batch[0]])]
     res = {vs: [] for vs in combos}
     stats = {}
     same = {}
