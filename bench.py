@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=0,
                     help="hrt_kernel: 0 auto, 1 literal, 2 brute, 3 brute_lds, 4 bundle, 5 bundle_cull")
     ap.add_argument("--row-tile", type=int, default=16)
+    ap.add_argument("--verify", action="store_true",
+                    help="N>1: rank 0 re-renders all frames on one full-frame context and compares the gathered frame")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo = host-staged gather (rehearsal on one GPU)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length (0 = skip)")
@@ -150,13 +152,20 @@ def main():
                 pmc = json.load(f)
             wl = pmc.get("workload", {})
             if (wl.get("scene"), wl.get("width"), wl.get("height"), wl.get("spp"), wl.get("bounces"),
-                    wl.get("variant")) == (args.scene, W, H, args.spp, args.bounces, args.variant) and world == 1:
-                traffic = pmc.get("hbm_bytes_per_trace_launch")
-                executed_flops = pmc.get("executed_fp32_flops_per_trace_launch")
+                    wl.get("variant")) == (args.scene, W, H, args.spp, args.bounces, args.variant):
+                per_test = pmc.get("executed_flops_per_reference_test")
+                if world == 1:
+                    traffic = pmc.get("hbm_bytes_per_trace_launch")
+                    executed_flops = pmc.get("executed_fp32_flops_per_trace_launch")
+                elif per_test:  # a rank's launch covers a row-tile subset: scale by its own work
+                    executed_flops = per_test * tests_per_launch
+                    if pmc.get("hbm_bytes_per_trace_launch"):
+                        traffic = pmc["hbm_bytes_per_trace_launch"] * ctx.local_rows / H
                 pmc_note = os.path.relpath(args.pmc_json, ROOT)
         # achieved = FP32 FLOPs the kernel executes per launch (hardware-counted by rocprofv3 on this
-        # deterministic workload: 64 * (2*FMA + MUL + ADD) wave-instructions) / the live launch time;
-        # without a matching PMC record, the reference-equivalent rate is reported instead.
+        # deterministic workload: 64 * (2*FMA + MUL + ADD) wave-instructions; N > 1: the same
+        # FLOPs-per-reference-test ratio applied to this rank's launches) / the live launch time.
+        # Without a matching PMC record the reference-equivalent rate is reported (see achieved_basis).
         achieved_tf = executed_flops / (kern_ms * 1e-3) / 1e12 if executed_flops else algorithmic_tf
         line = {
             "metric": "Mrays/s (island.obj 1080p 64spp 8-bounce path-trace segments per second)",
@@ -196,11 +205,35 @@ def main():
         }
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"], line["parity_sample"] = cpu_baseline(args, ctx, raytrace, camera)
+        if dist_on and args.verify:
+            line["gather_check"] = verify_gather(args, full, settings, camera, device, frame - 1)
         print(json.dumps(line), flush=True)
 
     ctx.close()
     if dist_on:
         dist.destroy_process_group()
+
+
+def verify_gather(args, full, settings, camera, device, last_frame):
+    """Rank 0: render frames 1..last_frame on one full-frame context (same accumulation sequence) and
+    compare its accumulator with the row-tile-gathered one byte for byte."""
+    import epq_raytracer_amd as E
+    from epq_raytracer_amd import _lib
+    W, H = args.width, args.height
+    ref_ctx = E.HrtContext((W, H), device=device, mode=_lib.MODE_RGBA8)
+    rt = E.RayTracePipeline(ref_ctx, (W, H), settings)
+    df = E.DiffusePipeline(ref_ctx, (W, H))
+    ref_ctx.set_option(_lib.OPT_KERNEL_VARIANT, args.variant)
+    rt.init()
+    df.next_frame(0, rt.image())
+    for k in range(1, last_frame + 1):
+        rt.compute(camera, k)
+        df.next_frame(k, rt.image())
+    ref = ref_ctx.read(_lib.IMG_ACCUM)
+    ref_ctx.close()
+    got = full.cpu().numpy()
+    return {"frames": last_frame, "bit_exact": bool(np.array_equal(got, ref)),
+            "pixels_differing": int(np.any(got != ref, axis=-1).sum())}
 
 
 def cpu_baseline(args, ctx, raytrace, camera):

@@ -88,6 +88,14 @@ def main():
         # the default (auto) trace kernel of the run
         k = max(res, key=lambda n: res[n].get("duration_s_median") or 0)
         d = res[k]
+        ref_tests = None  # the reference's triangle tests per launch (kbench JSON line of pass 1)
+        try:
+            with open(os.path.join(a.out, "p1.log")) as fh:
+                for line in fh:
+                    if line.startswith("{"):
+                        ref_tests = json.loads(line)["tri_tests"]
+        except (OSError, ValueError, KeyError):
+            pass
         with open(a.traffic_json, "w") as f:
             json.dump({"workload": wl, "kernel": k, "hbm_bytes_per_trace_launch": d.get("hbm_bytes"),
                        "hbm_read_bytes": d.get("hbm_read_bytes"), "hbm_write_bytes": d.get("hbm_write_bytes"),
@@ -95,6 +103,9 @@ def main():
                        "effective_clock_ghz": d.get("effective_clock_ghz"),
                        "executed_fp32_tflops": d.get("executed_fp32_tflops"),
                        "executed_fp32_flops_per_trace_launch": d.get("executed_fp32_flops"),
+                       "reference_tests_per_trace_launch": ref_tests,
+                       "executed_flops_per_reference_test": (d.get("executed_fp32_flops") / ref_tests
+                                                             if ref_tests and d.get("executed_fp32_flops") else None),
                        "valu_issue_utilisation": d.get("valu_issue_utilisation"),
                        "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes; separate --pmc passes, "
                                "kernel-trace only"}, f, indent=1)
