@@ -74,11 +74,14 @@ OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH = 1, 2, 3
 # hrt_kernel (include/hip_raytrace.h)
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
 KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull"}
+DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounce_iters", "bounce_considered",
+              "bounce_survivors", "bounce_lanes")
 
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).
 EXPORTED_SYMBOLS = (
     "hrt_abi_version", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate",
     "hrt_read_image", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
+    "hrt_get_diagnostics",
     "hrt_stream", "hrt_last_error",
     "hrt_host_create_rays", "hrt_host_view_matrix", "hrt_host_transform_meshes",
     "hrt_obj_load", "hrt_obj_num_meshes", "hrt_obj_mesh", "hrt_obj_free",
@@ -118,6 +121,7 @@ def load() -> ctypes.CDLL:
         "hrt_synchronize": (c_int32, [P]),
         "hrt_get_stats": (c_int32, [P, POINTER(Stats)]),
         "hrt_reset_stats": (c_int32, [P]),
+        "hrt_get_diagnostics": (c_int32, [P, P, c_uint32]),
         "hrt_set_option": (c_int32, [P, c_uint32, c_int64]),
         "hrt_stream": (c_void_p, [P]),
         "hrt_last_error": (c_char_p, [P]),

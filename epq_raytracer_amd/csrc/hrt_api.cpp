@@ -28,7 +28,7 @@ static_assert(offsetof(hrt_push_constants, height) == 120, "push layout");
 namespace {
 
 thread_local std::string g_create_error;
-constexpr int kNumCounters = 3;  // segments, triangle tests, wave steps
+constexpr int kNumCounters = 3 + HRT_NUM_DIAG;  // segments, triangle tests, wave steps, diagnostics
 
 struct EventPair {
   hipEvent_t start = nullptr, stop = nullptr;
@@ -62,6 +62,7 @@ struct hrt_context {
 
   int variant = 0;
   bool counters_on = true;
+  bool diag_on = false;
   uint32_t sec_batch = 48;
 
   std::vector<EventPair> event_pool;     // reusable
@@ -303,6 +304,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.img8 = ctx->trace8;
   p.img32 = ctx->trace32;
   p.counters = ctx->counters_on ? ctx->counters : nullptr;
+  p.diag = ctx->diag_on ? ctx->counters + 3 : nullptr;
   p.pc = *pc;
   p.local_rows = ctx->local_rows;
   p.row_tile = ctx->row_tile;
@@ -408,7 +410,7 @@ extern "C" hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out) {
   hrt_status st = hrt_synchronize(ctx);
   if (st != HRT_OK) return st;
   if ((st = harvest_events(ctx)) != HRT_OK) return st;
-  unsigned long long c[kNumCounters] = {0, 0, 0};
+  unsigned long long c[kNumCounters] = {};
   HRT_HIP(ctx, hipMemcpy(c, ctx->counters, sizeof c, hipMemcpyDeviceToHost));
   out->segments = c[0];
   out->tri_tests = c[1];
@@ -417,6 +419,16 @@ extern "C" hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out) {
   out->wave_steps = c[2];
   out->last_trace_ms = ctx->last_ms;
   out->total_trace_ms = ctx->total_ms;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_get_diagnostics(hrt_context* ctx, uint64_t* out, uint32_t count) {
+  if (!ctx || !out || count > HRT_NUM_DIAG) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = hrt_synchronize(ctx);
+  if (st != HRT_OK) return st;
+  unsigned long long c[kNumCounters] = {};
+  HRT_HIP(ctx, hipMemcpy(c, ctx->counters, sizeof c, hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < count; ++i) out[i] = c[3 + i];
   return HRT_OK;
 }
 
@@ -441,7 +453,9 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       ctx->variant = (int)value;
       return HRT_OK;
     case HRT_OPT_COUNTERS:
+      if (value < 0 || value > 2) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "counters option must be 0, 1 or 2");
       ctx->counters_on = value != 0;
+      ctx->diag_on = value == 2;
       return HRT_OK;
     case HRT_OPT_SECONDARY_BATCH:
       if (value < 1 || value > 64) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "secondary batch must be in [1, 64]");

@@ -16,7 +16,8 @@ struct TraceParams {
   const hrt_mesh* meshes;
   uint32_t* img8;                // local_rows x W packed RGBA8 (RGBA8 mode) or nullptr
   float4* img32;                 // local_rows x W float4 (RGBA32F mode) or nullptr
-  unsigned long long* counters;  // [0] segments, [1] triangle tests; nullptr = off
+  unsigned long long* counters;  // [0] segments, [1] triangle tests, [2] wave steps; nullptr = off
+  unsigned long long* diag;      // HRT_OPT_COUNTERS = 2: cull diagnostics (HRT_DIAG_*), else nullptr
   hrt_push_constants pc;
   uint32_t local_rows, row_tile, part_index, part_count;
   uint32_t n_tris;               // uploaded triangle count (LDS staging)

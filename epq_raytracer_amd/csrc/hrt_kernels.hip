@@ -477,6 +477,12 @@ struct Bundle {
   float c_lo, c_hi, s_hi;
 };
 
+// Wave-uniform cull diagnostics (HRT_OPT_COUNTERS = 2), flushed once per wave.
+struct Diag {
+  uint32_t prim_iters = 0, prim_considered = 0, prim_survivors = 0;
+  uint32_t sec_iters = 0, sec_considered = 0, sec_survivors = 0, sec_lanes = 0;
+};
+
 __device__ __forceinline__ float wave_min_all(float v) {  // all 64 lanes active
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
@@ -537,7 +543,7 @@ __device__ __forceinline__ void primary_exact(const float4* __restrict__ ct, uin
 
 // Primary segments of the lanes with prim == true.  Called with ALL 64 lanes of the wave active.
 __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TraceParams& P, bool prim, f3 o, f3 d,
-                                                 uint32_t& tests, Closest& c) {
+                                                 uint32_t& tests, Closest& c, Diag& dg) {
   const hrt_push_constants& pc = P.pc;
   const Bundle b = make_bundle(prim, d);
   spheres_first(sc, pc, prim, o, d, c);
@@ -563,6 +569,10 @@ __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TracePar
         keep = !rej;
       }
       unsigned long long mask = __ballot(keep);
+      if (P.diag) {
+        dg.prim_considered += min(64u, k1 - base);
+        dg.prim_survivors += (uint32_t)__popcll(mask);
+      }
       while (mask) {
         const uint32_t kk = base + (uint32_t)__builtin_ctzll(mask);
         mask &= mask - 1ull;
@@ -585,7 +595,7 @@ __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TracePar
 // Lane j bounds triangle base+j; survivors (buffer order) get the exact per-lane two-stage test.
 // Called with ALL 64 lanes active.
 __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const TraceParams& P, bool sec, f3 o, f3 d,
-                                                      uint32_t& tests, Closest& c) {
+                                                      uint32_t& tests, Closest& c, Diag& dg) {
   const hrt_push_constants& pc = P.pc;
   const float inf = __builtin_inff();
   const f3 lo = mk(wave_min_all(sec ? o.x : inf), wave_min_all(sec ? o.y : inf), wave_min_all(sec ? o.z : inf));
@@ -621,6 +631,10 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
         keep = !(s1 | r1);
       }
       unsigned long long mask = __ballot(keep);
+      if (P.diag) {
+        dg.sec_considered += min(64u, k1 - base);
+        dg.sec_survivors += (uint32_t)__popcll(mask);
+      }
       while (mask) {
         const uint32_t kk = base + (uint32_t)__builtin_ctzll(mask);
         mask &= mask - 1ull;
@@ -657,6 +671,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   Path p;
   p.bounce = pc.max_bounces + 1;
   bool done = !active;
+  Diag dg;
   while (__any(!done)) {
     if (!done && p.bounce > pc.max_bounces) {
       if (sample >= pc.num_samples) {
@@ -674,10 +689,15 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     const bool run_sec = nwait > 0 && (nwait >= P.sec_batch || !any_prim);
     const bool sec = waiting && run_sec;
     Closest c{kFltMax, 0, 0u, 0u};
-    if (any_prim) world_hit_bundle(sc, P, prim, p.pos, p.dir, tests, c);
+    if (P.diag) {
+      dg.prim_iters += any_prim ? 1u : 0u;
+      dg.sec_iters += run_sec ? 1u : 0u;
+      dg.sec_lanes += run_sec ? nwait : 0u;
+    }
+    if (any_prim) world_hit_bundle(sc, P, prim, p.pos, p.dir, tests, c, dg);
     if (run_sec) {
       if constexpr (BounceCull) {
-        world_hit_bounce_cull(sc, P, sec, p.pos, p.dir, tests, c);
+        world_hit_bounce_cull(sc, P, sec, p.pos, p.dir, tests, c, dg);
       } else {
         if (sec) c = world_hit_brute(sc, src, pc, p.pos, p.dir, tests);
       }
@@ -697,6 +717,15 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     store_pixel(P, x, lr, colour);
   }
   flush_counters(P, segs, tests);
+  if (P.diag && (threadIdx.x & 63) == 0) {
+    atomicAdd(&P.diag[0], (unsigned long long)dg.prim_iters);
+    atomicAdd(&P.diag[1], (unsigned long long)dg.prim_considered);
+    atomicAdd(&P.diag[2], (unsigned long long)dg.prim_survivors);
+    atomicAdd(&P.diag[3], (unsigned long long)dg.sec_iters);
+    atomicAdd(&P.diag[4], (unsigned long long)dg.sec_considered);
+    atomicAdd(&P.diag[5], (unsigned long long)dg.sec_survivors);
+    atomicAdd(&P.diag[6], (unsigned long long)dg.sec_lanes);
+  }
 }
 
 __global__ __launch_bounds__(256) void trace_bundle(TraceParams P) {

@@ -145,6 +145,12 @@ class HrtContext:
         self._check(self.lib.hrt_get_stats(self.handle, ctypes.byref(s)), "hrt_get_stats")
         return s
 
+    def diagnostics(self) -> dict:
+        """Cull diagnostics (needs set_option(OPT_COUNTERS, 2) before the traces)."""
+        out = np.zeros(len(_lib.DIAG_NAMES), np.uint64)
+        self._check(self.lib.hrt_get_diagnostics(self.handle, _lib.ptr(out), len(out)), "hrt_get_diagnostics")
+        return dict(zip(_lib.DIAG_NAMES, (int(v) for v in out)))
+
     def reset_stats(self):
         self._check(self.lib.hrt_reset_stats(self.handle), "hrt_reset_stats")
 

@@ -162,12 +162,25 @@ typedef enum hrt_kernel {
 typedef enum hrt_option {
   /* trace kernel variant (hrt_kernel), default HRT_KERNEL_AUTO */
   HRT_OPT_KERNEL_VARIANT = 1,
-  /* 1 = count segments / triangle tests on the device (default 1; 0 removes the counters' cost) */
+  /* 1 = count segments / triangle tests on the device (default); 0 = off; 2 = also the bundle
+   * kernels' cull diagnostics (hrt_get_diagnostics) */
   HRT_OPT_COUNTERS = 2,
   /* bundle kernel: a wave runs its bounce (non-primary) segments once this many lanes wait for one,
    * or when no lane has a primary segment left (1..64, default 48; results do not depend on it) */
   HRT_OPT_SECONDARY_BATCH = 3
 } hrt_option;
+
+/* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */
+typedef enum hrt_diag {
+  HRT_DIAG_PRIMARY_ITERS = 0,      /* wave iterations that ran the primary bundle path */
+  HRT_DIAG_PRIMARY_CONSIDERED = 1, /* camera-facing triangles bounded (per wave) */
+  HRT_DIAG_PRIMARY_SURVIVORS = 2,  /* ... of which survived the bundle cull */
+  HRT_DIAG_BOUNCE_ITERS = 3,       /* wave iterations that ran a bounce batch */
+  HRT_DIAG_BOUNCE_CONSIDERED = 4,  /* triangles bounded by the bounce pre-cull (per wave) */
+  HRT_DIAG_BOUNCE_SURVIVORS = 5,   /* ... of which survived */
+  HRT_DIAG_BOUNCE_LANES = 6,       /* lanes in bounce batches */
+  HRT_NUM_DIAG = 7
+} hrt_diag;
 
 uint32_t hrt_abi_version(void);
 
@@ -196,6 +209,7 @@ hrt_status hrt_get_layout(const hrt_context* ctx, hrt_layout* out);
 hrt_status hrt_synchronize(hrt_context* ctx);
 hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out); /* synchronizes */
 hrt_status hrt_reset_stats(hrt_context* ctx);
+hrt_status hrt_get_diagnostics(hrt_context* ctx, uint64_t* out, uint32_t count); /* synchronizes */
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
 /* HIP stream the context's work is ordered on (hipStream_t), for callers that interoperate. */

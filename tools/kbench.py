@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--json", default=None)
     ap.add_argument("--no-ref", action="store_true", help="skip the literal-kernel reference frame")
+    ap.add_argument("--diag", action="store_true", help="also print the bundle kernels' cull diagnostics")
     ap.add_argument("--sec-batch", type=int, nargs="+", default=[48], help="HRT_OPT_SECONDARY_BATCH values to sweep")
     a = ap.parse_args()
     W, H = (int(v) for v in a.size.split("x"))
@@ -56,6 +57,20 @@ def main():
             stats[(v, sb)] = (st.segments, st.tri_tests, st.wave_steps)
             if r == 0:
                 same[(v, sb)] = None if ref is None else bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
+    if a.diag:
+        for v in a.variants:
+            if v in (0, 4, 5):
+                ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
+                ctx.set_option(_lib.OPT_COUNTERS, 2)
+                ctx.reset_stats()
+                ctx.trace(pc)
+                d = ctx.diagnostics()
+                d["variant"] = v
+                d["primary_survival"] = d["primary_survivors"] / max(d["primary_considered"], 1)
+                d["bounce_survival"] = d["bounce_survivors"] / max(d["bounce_considered"], 1)
+                d["bounce_lanes_per_iter"] = d["bounce_lanes"] / max(d["bounce_iters"], 1)
+                print(json.dumps(d), flush=True)
+                ctx.set_option(_lib.OPT_COUNTERS, 1)
     out = []
     for v, sb in combos:
         ms = np.array(res[(v, sb)])
