@@ -70,18 +70,21 @@ STATUS_NAMES = {0: "HRT_OK", 1: "HRT_ERR_INVALID_ARGUMENT", 2: "HRT_ERR_NO_DEVIC
 MODE_RGBA8, MODE_RGBA32F = 0, 1
 IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
-OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH = 1, 2, 3
+OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
 # hrt_kernel (include/hip_raytrace.h)
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
-KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull"}
+KERNEL_BUNDLE_BVH = 6
+KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull", 6: "bundle_bvh"}
 DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounce_iters", "bounce_considered",
-              "bounce_survivors", "bounce_lanes")
+              "bounce_survivors", "bounce_lanes", "bvh_visits", "bvh_prim_tests", "bvh_band_tests", "primary_cycles", "bounce_cycles",
+              "shade_cycles")
+SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh_built", "bvh_band_entries")
 
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).
 EXPORTED_SYMBOLS = (
     "hrt_abi_version", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate",
     "hrt_read_image", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
-    "hrt_get_diagnostics",
+    "hrt_get_diagnostics", "hrt_get_scene_info",
     "hrt_stream", "hrt_last_error",
     "hrt_host_create_rays", "hrt_host_view_matrix", "hrt_host_transform_meshes",
     "hrt_obj_load", "hrt_obj_num_meshes", "hrt_obj_mesh", "hrt_obj_free",
@@ -104,10 +107,11 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+    path = os.environ.get("HRT_LIB", LIB_PATH)  # A/B builds of the same ABI (tools/kbench.py experiments)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                            " or `make -C epq_raytracer_amd/csrc` (no CPU fallback exists)")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     P = c_void_p
     sig = {
         "hrt_abi_version": (c_uint32, []),
@@ -122,6 +126,7 @@ def load() -> ctypes.CDLL:
         "hrt_get_stats": (c_int32, [P, POINTER(Stats)]),
         "hrt_reset_stats": (c_int32, [P]),
         "hrt_get_diagnostics": (c_int32, [P, P, c_uint32]),
+        "hrt_get_scene_info": (c_int32, [P, P, c_uint32]),
         "hrt_set_option": (c_int32, [P, c_uint32, c_int64]),
         "hrt_stream": (c_void_p, [P]),
         "hrt_last_error": (c_char_p, [P]),

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "hip_raytrace.h"
+#include "hrt_bvh.h"
 #include "hrt_kernels.h"
 
 static_assert(sizeof(hrt_material) == 48, "std430 RayTracingMaterial");
@@ -59,6 +60,13 @@ struct hrt_context {
   uint32_t cam_capacity = 0;      // sum of mesh lengths
   float4* cam_tris = nullptr;     // compacted camera-facing records (64 B each)
   float4* cam_cull = nullptr;     // bundle-cull records (80 B each)
+  float4* bvh_nodes = nullptr;    // BUNDLE_BVH hierarchy (hrt_bvh.h), built by hrt_set_scene
+  float4* bvh_prims = nullptr;
+  float4* bvh_irregular = nullptr;
+  uint32_t* bvh_band_off = nullptr;
+  float4* bvh_band = nullptr;
+  uint32_t bvh_info[HRT_NUM_SCENE_INFO] = {};  // hrt_get_scene_info
+  uint32_t bvh_leaf = 4;
 
   int variant = 0;
   bool counters_on = true;
@@ -272,6 +280,33 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_tris, (size_t)(cap ? cap : 1) * 64));
   HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_cull, (size_t)(cap ? cap : 1) * 80));
   ctx->cam_capacity = (uint32_t)cap;
+  // bounce-segment hierarchy (BUNDLE_BVH)
+  hrt::BvhHost bvh;
+  const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, ctx->bvh_leaf, bvh);
+  free_dev(ctx->bvh_nodes);
+  free_dev(ctx->bvh_prims);
+  free_dev(ctx->bvh_irregular);
+  free_dev(ctx->bvh_band_off);
+  free_dev(ctx->bvh_band);
+  if (built) {
+    auto up = [&](auto*& dst, const auto& v) -> hrt_status {
+      const size_t bytes = v.size() * sizeof(v[0]);
+      HRT_HIP(ctx, hipMalloc((void**)&dst, bytes ? bytes : 16));
+      if (bytes) HRT_HIP(ctx, hipMemcpyAsync(dst, v.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+      return HRT_OK;
+    };
+    if ((st = up(ctx->bvh_nodes, bvh.nodes)) != HRT_OK) return st;
+    if ((st = up(ctx->bvh_prims, bvh.prims)) != HRT_OK) return st;
+    if ((st = up(ctx->bvh_irregular, bvh.irregular)) != HRT_OK) return st;
+    if ((st = up(ctx->bvh_band_off, bvh.band_off)) != HRT_OK) return st;
+    if ((st = up(ctx->bvh_band, bvh.band_list)) != HRT_OK) return st;  // 16 B entries
+  }
+  ctx->bvh_info[0] = bvh.n_nodes;
+  ctx->bvh_info[1] = bvh.n_prims;
+  ctx->bvh_info[2] = bvh.n_irregular;
+  ctx->bvh_info[3] = bvh.n_never;
+  ctx->bvh_info[4] = built ? 1u : 0u;
+  ctx->bvh_info[5] = (uint32_t)(bvh.band_list.size() / 4);
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
   ctx->n_rays = n_rays;
   ctx->n_spheres = n_spheres;
@@ -317,6 +352,13 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.cam_tris = ctx->cam_tris;
   p.cam_cull = ctx->cam_cull;
   p.sec_batch = ctx->sec_batch;
+  p.bvh_nodes = ctx->bvh_info[4] ? ctx->bvh_nodes : nullptr;
+  p.bvh_prims = ctx->bvh_prims;
+  p.bvh_irregular = ctx->bvh_irregular;
+  p.bvh_band_off = ctx->bvh_band_off;
+  p.bvh_band = ctx->bvh_band;
+  p.bvh_n_nodes = ctx->bvh_info[0];
+  p.bvh_n_irregular = ctx->bvh_info[2];
   const int variant = ctx->variant;
 
   EventPair ev;
@@ -432,6 +474,12 @@ extern "C" hrt_status hrt_get_diagnostics(hrt_context* ctx, uint64_t* out, uint3
   return HRT_OK;
 }
 
+extern "C" hrt_status hrt_get_scene_info(hrt_context* ctx, uint32_t* out, uint32_t count) {
+  if (!ctx || !out || count > HRT_NUM_SCENE_INFO) return HRT_ERR_INVALID_ARGUMENT;
+  for (uint32_t i = 0; i < count; ++i) out[i] = ctx->bvh_info[i];
+  return HRT_OK;
+}
+
 extern "C" hrt_status hrt_reset_stats(hrt_context* ctx) {
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   hrt_status st = hrt_synchronize(ctx);
@@ -448,8 +496,8 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   switch (key) {
     case HRT_OPT_KERNEL_VARIANT:
-      if (value < HRT_KERNEL_AUTO || value > HRT_KERNEL_BUNDLE_CULL)
-        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be an hrt_kernel value (0..5)");
+      if (value < HRT_KERNEL_AUTO || value > HRT_KERNEL_BUNDLE_BVH)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be an hrt_kernel value (0..6)");
       ctx->variant = (int)value;
       return HRT_OK;
     case HRT_OPT_COUNTERS:
@@ -460,6 +508,11 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
     case HRT_OPT_SECONDARY_BATCH:
       if (value < 1 || value > 64) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "secondary batch must be in [1, 64]");
       ctx->sec_batch = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_BVH_LEAF_SIZE:
+      if (value < 1 || value > hrt::kBvhMaxLeafCount)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "BVH leaf size must be in [1, 16]");
+      ctx->bvh_leaf = (uint32_t)value;
       return HRT_OK;
     default:
       return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "unknown option key");

@@ -1,0 +1,367 @@
+// hrt_bvh.cpp -- binned-SAH build of the bounce-segment BVH (hrt_bvh.h).  Host C++, run by
+// hrt_set_scene; all bounds are computed in double and rounded outward to float so that the trace
+// kernel's cull tests are conservative (DESIGN.md "BVH cull").
+#include "hrt_bvh.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+namespace hrt {
+namespace {
+
+struct V3 {
+  double x, y, z;
+};
+inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 operator*(V3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+inline double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline double norm(V3 a) { return std::sqrt(dot(a, a)); }
+inline double comp(V3 a, int k) { return k == 0 ? a.x : (k == 1 ? a.y : a.z); }
+inline V3 ld(const float* p) { return {p[0], p[1], p[2]}; }
+
+struct Box {
+  V3 lo{HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi{-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+  void grow(V3 p) {
+    lo = {std::min(lo.x, p.x), std::min(lo.y, p.y), std::min(lo.z, p.z)};
+    hi = {std::max(hi.x, p.x), std::max(hi.y, p.y), std::max(hi.z, p.z)};
+  }
+  void grow(const Box& b) {
+    grow(b.lo);
+    grow(b.hi);
+  }
+  double area() const {
+    if (lo.x > hi.x) return 0.0;
+    const V3 e = hi - lo;
+    return 2.0 * (e.x * e.y + e.y * e.z + e.z * e.x);
+  }
+};
+
+// One regular (mesh, triangle) entry.
+struct Entry {
+  Box box;
+  V3 centroid;
+  V3 nhat;         // n_rec / |n_rec|
+  double g;        // max(|e1|, |e2|) / |n_rec|
+  double rho;      // |n_rec - e1 x e2| / |n_rec|
+  double ext;      // largest per-axis extent of the triangle
+  uint32_t key, mesh, index;
+};
+
+float round_down(double v) {
+  float f = (float)v;
+  if ((double)f > v) f = std::nextafter(f, -HUGE_VALF);
+  return f;
+}
+float round_up(double v) {
+  float f = (float)v;
+  if ((double)f < v) f = std::nextafter(f, HUGE_VALF);
+  return f;
+}
+float bits_f(uint32_t u) {
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+struct Builder {
+  std::vector<Entry>& e;
+  uint32_t leaf_size;
+  BvhHost& out;
+
+  void emit_prim(const Entry& en, const hrt_triangle* tris) {
+    const hrt_triangle& t = tris[en.index];
+    const float rec[16] = {t.a[0], t.a[1], t.a[2], bits_f(en.key),
+                           t.edge_one[0], t.edge_one[1], t.edge_one[2], bits_f(en.mesh),
+                           t.edge_two[0], t.edge_two[1], t.edge_two[2], bits_f(en.index),
+                           t.normal[0], t.normal[1], t.normal[2], 0.0f};
+    out.prims.insert(out.prims.end(), rec, rec + 16);
+  }
+
+  void build(uint32_t b, uint32_t n, const hrt_triangle* tris) {
+    const uint32_t node = out.n_nodes++;
+    out.nodes.resize((size_t)out.n_nodes * 16, 0.0f);
+    Box box, cbox;
+    V3 axis{0, 0, 0};
+    double g = 0, rho = 0, ext = 0;
+    for (uint32_t i = b; i < b + n; ++i) {
+      box.grow(e[i].box);
+      cbox.grow(e[i].centroid);
+      axis = axis + e[i].nhat;
+      g = std::max(g, e[i].g);
+      rho = std::max(rho, e[i].rho);
+      ext = std::max(ext, e[i].ext);
+    }
+    // normal cone around the mean direction
+    double cphi = 0.0, sphi = 1.0;
+    const double an = norm(axis);
+    if (an > 1e-9) {
+      axis = axis * (1.0 / an);
+      double phi = 0.0;
+      for (uint32_t i = b; i < b + n; ++i) phi = std::max(phi, std::acos(std::max(-1.0, std::min(1.0, dot(axis, e[i].nhat)))));
+      phi += 1e-6;
+      if (phi < 1.5707963267948966) {
+        cphi = std::cos(phi);
+        sphi = std::sin(phi);
+      }
+    }
+    if (!(cphi > 0.0)) {
+      axis = {1.0, 0.0, 0.0};
+      cphi = 0.0;
+      sphi = 1.0;
+    }
+
+    bool leaf = n <= leaf_size;
+    uint32_t mid = b + n / 2;
+    if (!leaf) {
+      // binned SAH over the centroid box, 16 bins per axis
+      constexpr int kBins = 16;
+      double best = HUGE_VAL;
+      int best_axis = -1, best_split = 0;
+      for (int k = 0; k < 3; ++k) {
+        const double lo = comp(cbox.lo, k), hi = comp(cbox.hi, k);
+        if (!(hi > lo)) continue;
+        Box bins[kBins];
+        uint32_t cnt[kBins] = {};
+        const double scale = kBins / (hi - lo);
+        for (uint32_t i = b; i < b + n; ++i) {
+          int j = (int)((comp(e[i].centroid, k) - lo) * scale);
+          j = std::min(kBins - 1, std::max(0, j));
+          bins[j].grow(e[i].box);
+          cnt[j]++;
+        }
+        double right_area[kBins];
+        uint32_t right_cnt[kBins];
+        Box acc;
+        uint32_t c = 0;
+        for (int j = kBins - 1; j > 0; --j) {
+          acc.grow(bins[j]);
+          c += cnt[j];
+          right_area[j] = acc.area();
+          right_cnt[j] = c;
+        }
+        Box left;
+        uint32_t lc = 0;
+        for (int j = 1; j < kBins; ++j) {
+          left.grow(bins[j - 1]);
+          lc += cnt[j - 1];
+          if (lc == 0 || right_cnt[j] == 0) continue;
+          const double cost = left.area() * lc + right_area[j] * right_cnt[j];
+          if (cost < best) {
+            best = cost;
+            best_axis = k;
+            best_split = j;
+          }
+        }
+      }
+      if (best_axis >= 0) {
+        const double lo = comp(cbox.lo, best_axis), hi = comp(cbox.hi, best_axis);
+        const double scale = kBins / (hi - lo);
+        auto it = std::partition(e.begin() + b, e.begin() + b + n, [&](const Entry& x) {
+          int j = (int)((comp(x.centroid, best_axis) - lo) * scale);
+          j = std::min(kBins - 1, std::max(0, j));
+          return j < best_split;
+        });
+        mid = (uint32_t)(it - e.begin());
+      }
+      if (mid <= b || mid >= b + n) mid = b + n / 2;  // coincident centroids: split the range
+    }
+
+    float* r = &out.nodes[(size_t)node * 16];
+    r[0] = round_down(box.lo.x);
+    r[1] = round_down(box.lo.y);
+    r[2] = round_down(box.lo.z);
+    r[3] = round_up(ext * (1.0 + 1e-12));
+    r[4] = round_up(box.hi.x);
+    r[5] = round_up(box.hi.y);
+    r[6] = round_up(box.hi.z);
+    r[7] = round_up(g * (1.0 + 1e-9));
+    r[8] = (float)axis.x;
+    r[9] = (float)axis.y;
+    r[10] = (float)axis.z;
+    r[11] = (float)cphi;
+    r[12] = (float)sphi;
+    r[13] = round_up(rho + 1e-12);
+    if (leaf) {
+      r[14] = bits_f(out.n_prims | (n << 27));
+      for (uint32_t i = b; i < b + n; ++i) emit_prim(e[i], tris);
+      out.n_prims += n;
+    } else {
+      r[14] = bits_f(0u);
+      build(b, mid - b, tris);
+      build(mid, b + n - mid, tris);
+    }
+    out.nodes[(size_t)node * 16 + 15] = bits_f(out.n_nodes);  // escape: first node after the subtree
+  }
+};
+
+bool finite3(const float* p) { return std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]); }
+
+// Cube-map direction of face f (2 * major axis + negative) at tangent coordinates (u, v); the trace
+// kernel's dir_cell inverts this (u, v = the two minor components over the major one).
+V3 face_dir(int f, double u, double v) {
+  const double s = (f & 1) ? -1.0 : 1.0;
+  switch (f >> 1) {
+    case 0: return {s, u, v};
+    case 1: return {v, s, u};
+    default: return {u, v, s};
+  }
+}
+
+struct Cone {
+  V3 c;
+  double cr, sr;  // cos, sin of the cap radius
+};
+
+// Cap containing every direction of the cell [u0, u1] x [v0, v1] of face f (a convex spherical quad,
+// so the farthest point from the centre is a corner), widened by 1e-4 rad for the kernel's rounding.
+Cone cell_cone(int f, double u0, double u1, double v0, double v1) {
+  V3 c = face_dir(f, 0.5 * (u0 + u1), 0.5 * (v0 + v1));
+  c = c * (1.0 / norm(c));
+  double r = 0.0;
+  const double us[2] = {u0, u1}, vs[2] = {v0, v1};
+  for (double u : us)
+    for (double v : vs) {
+      V3 d = face_dir(f, u, v);
+      d = d * (1.0 / norm(d));
+      r = std::max(r, std::acos(std::max(-1.0, std::min(1.0, dot(c, d)))));
+    }
+  r += 1e-4;
+  return {c, std::cos(r), std::sin(r)};
+}
+
+// Is d.nhat in the grazing band (-kBandTau - 1e-5, 2e-5) for some d in the cap?  With
+// theta = angle(c, nhat): d.nhat ranges over [cos(min(pi, theta + r)), cos(max(0, theta - r))].
+bool cone_hits_band(const Cone& k, V3 nhat) {
+  const double x = std::max(-1.0, std::min(1.0, dot(k.c, nhat)));
+  const double y = std::sqrt(std::max(0.0, 1.0 - x * x));
+  const double hi = (x >= k.cr) ? 1.0 : x * k.cr + y * k.sr;
+  const double lo = (x <= -k.cr) ? -1.0 : x * k.cr - y * k.sr;
+  return hi > -((double)kBandTau + 1e-5) && lo < 2e-5;
+}
+
+void build_band_lists(BvhHost& out) {
+  std::vector<V3> nh(out.n_prims);
+  for (uint32_t k = 0; k < out.n_prims; ++k) {
+    const V3 n = ld(&out.prims[(size_t)k * 16 + 12]);
+    nh[k] = n * (1.0 / norm(n));
+  }
+  constexpr int kCoarse = 8, kSub = kDirRes / kCoarse;
+  out.band_off.assign(kDirCells + 1, 0);
+  std::vector<std::vector<uint32_t>> lists(kDirCells);
+  // one task per coarse cell: its candidates, then its kSub x kSub fine cells
+  auto task = [&](int t) {
+    const int f = t / (kCoarse * kCoarse), cu = (t / kCoarse) % kCoarse, cv = t % kCoarse;
+    const Cone kc = cell_cone(f, -1.0 + 2.0 * cu / kCoarse, -1.0 + 2.0 * (cu + 1) / kCoarse,
+                              -1.0 + 2.0 * cv / kCoarse, -1.0 + 2.0 * (cv + 1) / kCoarse);
+    std::vector<uint32_t> coarse;
+    for (uint32_t k = 0; k < out.n_prims; ++k)
+      if (cone_hits_band(kc, nh[k])) coarse.push_back(k);
+    for (int su = 0; su < kSub; ++su) {
+      for (int sv = 0; sv < kSub; ++sv) {
+        const int iu = cu * kSub + su, iv = cv * kSub + sv;
+        const Cone fc = cell_cone(f, -1.0 + 2.0 * iu / kDirRes, -1.0 + 2.0 * (iu + 1) / kDirRes,
+                                  -1.0 + 2.0 * iv / kDirRes, -1.0 + 2.0 * (iv + 1) / kDirRes);
+        std::vector<uint32_t>& l = lists[((size_t)f * kDirRes + iu) * kDirRes + iv];
+        for (uint32_t k : coarse)
+          if (cone_hits_band(fc, nh[k])) l.push_back(k);
+      }
+    }
+  };
+  constexpr int kTasks = 6 * kCoarse * kCoarse;
+  const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::atomic<int> next{0};
+  auto worker = [&]() {
+    for (int t; (t = next.fetch_add(1)) < kTasks;) task(t);
+  };
+  std::vector<std::thread> pool;
+  for (unsigned i = 1; i < nthreads && out.n_prims > 64; ++i) pool.emplace_back(worker);
+  worker();
+  for (auto& th : pool) th.join();
+  for (int c = 0; c < kDirCells; ++c) out.band_off[c + 1] = out.band_off[c] + (uint32_t)lists[c].size();
+  out.band_list.reserve((size_t)out.band_off[kDirCells] * 4);
+  for (int c = 0; c < kDirCells; ++c) {
+    for (uint32_t k : lists[c]) {
+      // (n / |n|, prim index bits): the kernel's pre-check of d.n^ against the band
+      const float* n = &out.prims[(size_t)k * 16 + 12];
+      const double inv = 1.0 / norm(ld(n));
+      const float e[4] = {(float)(n[0] * inv), (float)(n[1] * inv), (float)(n[2] * inv), bits_f(k)};
+      uint32_t w[4];
+      std::memcpy(w, e, 16);
+      out.band_list.insert(out.band_list.end(), w, w + 4);
+    }
+  }
+}
+
+}  // namespace
+
+bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
+               uint32_t leaf_size, BvhHost& out) {
+  out = BvhHost{};
+  if (n_meshes > kBvhMaxMeshes) return false;
+  uint64_t total = 0;
+  for (uint32_t m = 0; m < n_meshes; ++m) total += meshes[m].len;
+  if (total > kBvhMaxEntries) return false;
+  leaf_size = std::max(1u, std::min(leaf_size, kBvhMaxLeafCount));
+  std::vector<Entry> entries;
+  entries.reserve(total);
+  uint32_t key = 1;
+  for (uint32_t m = 0; m < n_meshes; ++m) {
+    for (uint32_t k = 0; k < meshes[m].len; ++k, ++key) {
+      const uint32_t i = meshes[m].first_index + k;
+      if (i >= n_tris) continue;  // hrt_set_scene validated the ranges
+      const hrt_triangle& t = tris[i];
+      if (t.normal[0] == 0.0f && t.normal[1] == 0.0f && t.normal[2] == 0.0f) {
+        out.n_never++;  // d.n is +-0 for every d: the reference's dn >= 0 rejects it (raytracing.glsl:219)
+        continue;
+      }
+      const V3 a = ld(t.a), e1 = ld(t.edge_one), e2 = ld(t.edge_two), n = ld(t.normal);
+      const V3 b = a + e1, c = a + e2;
+      const double nn = norm(n), l1 = norm(e1), l2 = norm(e2);
+      const double big = 1e18;
+      bool regular = finite3(t.a) && finite3(t.edge_one) && finite3(t.edge_two) && finite3(t.normal) &&
+                     nn >= 1e-25 && nn <= 1e30 && l1 <= big && l2 <= big;
+      for (int q = 0; q < 3 && regular; ++q)
+        regular = std::fabs(comp(a, q)) <= big && std::fabs(comp(b, q)) <= big && std::fabs(comp(c, q)) <= big;
+      double rho = 0.0;
+      if (regular) {
+        rho = norm(n - cross(e1, e2)) / nn + 1e-12;
+        regular = rho <= 1e-4;
+      }
+      if (!regular) {
+        const float rec[16] = {t.a[0], t.a[1], t.a[2], bits_f(key),
+                               t.edge_one[0], t.edge_one[1], t.edge_one[2], bits_f(m),
+                               t.edge_two[0], t.edge_two[1], t.edge_two[2], bits_f(i),
+                               t.normal[0], t.normal[1], t.normal[2], 0.0f};
+        out.irregular.insert(out.irregular.end(), rec, rec + 16);
+        out.n_irregular++;
+        continue;
+      }
+      Entry en;
+      en.box.grow(a);
+      en.box.grow(b);
+      en.box.grow(c);
+      en.centroid = (a + b + c) * (1.0 / 3.0);
+      en.nhat = n * (1.0 / nn);
+      en.g = std::max(l1, l2) / nn;
+      en.rho = rho;
+      en.ext = std::max({en.box.hi.x - en.box.lo.x, en.box.hi.y - en.box.lo.y, en.box.hi.z - en.box.lo.z});
+      en.key = key;
+      en.mesh = m;
+      en.index = i;
+      entries.push_back(en);
+    }
+  }
+  if (!entries.empty()) {
+    Builder bld{entries, leaf_size, out};
+    bld.build(0, (uint32_t)entries.size(), tris);
+  }
+  build_band_lists(out);
+  return true;
+}
+
+}  // namespace hrt

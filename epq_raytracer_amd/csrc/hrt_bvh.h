@@ -1,0 +1,59 @@
+// hrt_bvh.h -- host-built bounding volume hierarchy for bounce segments (HRT_KERNEL_BUNDLE_BVH).
+//
+// The reference scans every triangle of every mesh whose AABB test passes (raytracing.glsl:278-286);
+// the BVH only lets the trace kernel skip triangles it can PROVE the reference rejects for a given
+// ray, so results stay byte-identical (DESIGN.md "BVH cull" has the error analysis).  Each entry is
+// one (mesh m, triangle i) of the reference's scan with key = 1 + its scan position, which breaks
+// equal-distance ties exactly like the reference's strict '<' in scan order.
+#pragma once
+
+#include <stdint.h>
+
+#include <vector>
+
+#include "hip_raytrace.h"
+
+namespace hrt {
+
+// 16 floats per node:
+//   [0..2]  box lo (vertices a, a+e1, a+e2 of every triangle below, rounded outward)
+//   [3]     tri_ext: max over those triangles of their largest per-axis extent
+//   [4..6]  box hi
+//   [7]     G = max |e|max / |n|   (1 / length; conditioning of the barycentric numerators)
+//   [8..10] normal-cone axis c (unit)
+//   [11]    cos(phi)   (phi >= angle(c, n_i / |n_i|) for every triangle; (0, 1) = no cone)
+//   [12]    sin(phi)
+//   [13]    rho = max |n_i - e1_i x e2_i| / |n_i|   (record normal vs exact cross product)
+//   [14]    bits: leaf ? first_prim | count << 27 : 0
+//   [15]    bits: escape node (preorder successor that is not a descendant; n_nodes = end)
+// 16 floats per prim: (a, key bits) (e1, mesh bits) (e2, triangle index bits) (n, 0).
+//
+// Grazing band: the box cull's error bound needs |d.n^| >= kBandTau for front-facing triangles, so
+// every triangle with d.n^ in (-kBandTau, +2e-5) ("in the band" of d) is tested separately.  Ray
+// directions are binned on a cube map (face, iu, iv), kDirRes x kDirRes cells per face; band_list of a
+// cell holds every leaf prim that is in the band of SOME direction of that cell.
+struct BvhHost {
+  std::vector<float> nodes;
+  std::vector<float> prims;      // leaf-ordered regular triangles
+  std::vector<float> irregular;  // entries the analysis does not cover: tested for every bounce ray
+  std::vector<uint32_t> band_off;   // 6 kDirRes^2 + 1 offsets into band_list
+  std::vector<uint32_t> band_list;  // 4 words per entry: n^ (3 floats, rounded), prim index
+  uint32_t n_nodes = 0, n_prims = 0, n_irregular = 0, n_never = 0;  // never = zero normal (dn == 0)
+};
+
+constexpr float kBandTau = 3e-3f;
+constexpr int kDirRes = 64;
+constexpr int kDirCells = 6 * kDirRes * kDirRes;
+
+constexpr uint32_t kBvhMaxMeshes = 64;     // per-lane mesh filter is a 64-bit mask
+constexpr uint32_t kBvhMaxLeafCount = 16;  // leaf count lives in bits 27..31 of node word 14
+// The grazing-band lists hold ~450 entries (16 B) per triangle on the reference's meshes, so the
+// hierarchy is not built above this many (mesh, triangle) entries (~1.9 GB of band lists).
+constexpr uint64_t kBvhMaxEntries = 1u << 18;
+
+// Builds the hierarchy over every (mesh, triangle) entry of the scene.  Returns false (and leaves
+// `out` empty) when the scene has more than kBvhMaxMeshes meshes or kBvhMaxEntries entries.
+bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
+               uint32_t leaf_size, BvhHost& out);
+
+}  // namespace hrt

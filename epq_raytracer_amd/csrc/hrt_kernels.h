@@ -28,6 +28,13 @@ struct TraceParams {
   float4* cam_tris;              // 4 float4 per record: (ao, num_t) (e1, index bits) (e2, -) (n, -)
   float4* cam_cull;              // 5 float4 per record: bundle-cull linear forms + margins
   uint32_t sec_batch;            // bounce segments run once this many lanes of a wave wait (1..64)
+  // BUNDLE_BVH: bounce-segment hierarchy built by hrt_set_scene (hrt_bvh.h records); nullptr = none.
+  const float4* bvh_nodes;       // 4 float4 per node, preorder with escape indices
+  const float4* bvh_prims;       // 4 float4 per leaf triangle
+  const float4* bvh_irregular;   // 4 float4 per entry outside the analysis (tested for every ray)
+  const uint32_t* bvh_band_off;  // kDirCells + 1 offsets: grazing-band prims per direction cell
+  const float4* bvh_band;        // (n^, prim index bits) per entry
+  uint32_t bvh_n_nodes, bvh_n_irregular;
 };
 
 hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream);

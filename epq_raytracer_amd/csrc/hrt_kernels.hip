@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include "hip_raytrace.h"
+#include "hrt_bvh.h"
 #include "hrt_kernels.h"
 #include "hrt_math.h"
 
@@ -481,6 +482,8 @@ struct Bundle {
 struct Diag {
   uint32_t prim_iters = 0, prim_considered = 0, prim_survivors = 0;
   uint32_t sec_iters = 0, sec_considered = 0, sec_survivors = 0, sec_lanes = 0;
+  uint32_t bvh_visits = 0, bvh_prims = 0, bvh_band = 0;  // per lane (BUNDLE_BVH)
+  uint64_t cyc_prim = 0, cyc_sec = 0, cyc_shade = 0;  // shader clocks per wave and phase
 };
 
 __device__ __forceinline__ float wave_min_all(float v) {  // all 64 lanes active
@@ -645,12 +648,198 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
   }
 }
 
-// Fused loop of BUNDLE / BUNDLE_CULL.  Every lane stays in the loop until the whole wave is done, so
+// ---- BUNDLE_BVH: per-lane hierarchy traversal for bounce segments ----------------------------------
+// Each bounce lane walks the BVH (hrt_bvh.h) in preorder with escape indices (one register of
+// state).  For a triangle (a, e1, e2, n) and the lane's ray (o, d), |d| = 1 (DESIGN.md "BVH cull"):
+//   back     d.n^ >= 2e-5: the reference's dn = d.n rounds to > 0 and raytracing.glsl:219 rejects;
+//   band     -kBandTau - 1e-5 < d.n^ < 2e-5: grazing; the reference's arithmetic is rounding noise
+//            there and may accept anywhere in the triangle's plane, so these triangles are listed per
+//            cube-map direction cell (hrt_bvh.cpp build_band_lists) and every lane tests its cell's
+//            list exactly;
+//   front    d.n^ <= -tau with tau >= kBandTau: an accepted triangle's reference (u, v, w) >= 0 puts
+//            the exact intersection of the ray's line with the triangle's plane inside the triangle
+//            inflated by eta (barycentrics >= -eta), at a line parameter within rel*t + abs of the
+//            accepted dist, where
+//              eta = 6e + (1.01 rho + 3.2e + 18.4e G R) / (tau - rho - 4e-7)
+//              abs = 2.1 (4.2e + rho) R / (tau - rho - 4e-7),  rel = 2.1 (3.2e + rho) / (...) + 4e
+//            (e = 2^-24, R >= |o - a| over the node, G and rho from the node record).
+// So a node is skipped when its normal cone is entirely back-facing, or when the ray segment
+// t in [-abs, best (1 + rel) + abs] misses the node box grown by 2 eta tri_ext (plus coordinate
+// rounding), tau = max(kBandTau, -max over the cone of d.n^): no triangle below can then be
+// accepted with dist <= best except band triangles, which the band list covers.  Equal distances are
+// resolved by the scan key (first in the reference's mesh/index order wins).
+constexpr float kEps = 5.9604644775390625e-08f;  // 2^-24
+
+__device__ __forceinline__ void bvh_prim_test(const float4* __restrict__ pr, uint32_t k, unsigned long long mask, f3 o,
+                                              f3 d, Closest& c, uint32_t& bkey, float& best_k) {
+  const float4 A = pr[4 * k], B = pr[4 * k + 1];
+  const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
+  if (!((mask >> m) & 1ull)) return;  // mesh failed its (quirky) AABB test for this lane
+  const float4 N = pr[4 * k + 3];
+  const f3 n = mk(N.x, N.y, N.z);
+  const f3 ao = o - mk(A.x, A.y, A.z);
+  TriPre q;
+  q.num_t = dot(ao, n);
+  if (!(q.num_t > 0.0f)) return;
+  const float dn = dot(d, n);
+  if (!(dn < 0.0f)) return;
+  const float4 C = pr[4 * k + 2];
+  const f3 dao = cross(ao, d);
+  q.num_u = dot(mk(C.x, C.y, C.z), dao);
+  q.num_v = dot(mk(B.x, B.y, B.z), dao);
+  q.det = -dn;
+  if (pre_reject(q, best_k)) return;
+  const float inv_det = 1.0f / q.det;
+  const float dist = q.num_t * inv_det;
+  const float u = q.num_u * inv_det;
+  const float v = -q.num_v * inv_det;
+  const float w = 1.0f - u - v;
+  const uint32_t key = __builtin_bit_cast(uint32_t, A.w);
+  if (!(dist < 0.0f) && !(u < 0.0f) && !(v < 0.0f) && !(w < 0.0f) && dist > 0.001f &&
+      (dist < c.t || (dist == c.t && key < bkey))) {
+    c = Closest{dist, 2, __builtin_bit_cast(uint32_t, C.w), m};
+    bkey = key;
+    best_k = dist * kOnePlus;
+  }
+}
+
+// true when the node may hold a triangle the reference accepts for (o, d) with dist <= best.
+__device__ __forceinline__ bool bvh_node_visit(const float4& N0, const float4& N1, const float4& N2, const float4& N3,
+                                               f3 o, f3 d, f3 inv, float best) {
+  const float x = N2.x * d.x + N2.y * d.y + N2.z * d.z;  // cos(angle(d, axis)) within 2e-6
+  const float xa = fmaxf(fabsf(x) - 2e-6f, 0.0f);
+  const float s_up = __builtin_sqrtf(fmaxf(1.0f - xa * xa, 0.0f)) + 1e-6f;
+  const float xc = x * N2.w, ss = s_up * N3.x;
+  if (xc - ss - 1e-6f > 1e-5f) return false;  // back: every dn > 0
+  const float tau = fmaxf(kBandTau, -(xc + ss + 1e-6f));
+  const float rho = N3.y;  // <= 1e-4 (hrt_bvh.cpp: larger goes to the irregular list)
+  const float inv_tp = 1.02f / (tau - rho - 4e-7f);
+  const f3 lo = mk(N0.x, N0.y, N0.z), hi = mk(N1.x, N1.y, N1.z);
+  const f3 ctr = (lo + hi) * 0.5f, half = (hi - lo) * 0.5f;
+  const f3 oc = o - ctr;
+  const float R = (__builtin_sqrtf(dot(oc, oc)) + __builtin_sqrtf(dot(half, half))) * 1.0001f;
+  const float abs_t = 2.1f * (4.2f * kEps + rho) * R * inv_tp;
+  const float rel_t = 2.1f * (3.2f * kEps + rho) * inv_tp + 4.0f * kEps;
+  const float eta = 6.0f * kEps + (1.01f * rho + 3.2f * kEps + 18.4f * kEps * N1.w * R) * inv_tp;
+  const float coord = fmaxf(fmaxf(fabsf(ctr.x), fabsf(ctr.y)), fabsf(ctr.z)) +
+                      fmaxf(fmaxf(half.x, half.y), half.z);
+  const float mg = 2.02f * eta * N0.w + 4.0f * kEps * coord;
+  const float t_hi = best * (1.0f + rel_t) + abs_t;
+  const float tx0 = ((lo.x - mg) - o.x) * inv.x, tx1 = ((hi.x + mg) - o.x) * inv.x;
+  const float ty0 = ((lo.y - mg) - o.y) * inv.y, ty1 = ((hi.y + mg) - o.y) * inv.y;
+  const float tz0 = ((lo.z - mg) - o.z) * inv.z, tz1 = ((hi.z + mg) - o.z) * inv.z;
+  const float tn = fmaxf(fmaxf(-abs_t, fminf(tx0, tx1)), fmaxf(fminf(ty0, ty1), fminf(tz0, tz1)));
+  const float tf = fminf(fminf(t_hi, fmaxf(tx0, tx1)), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
+  return !((tn - fabsf(tn) * 1e-6f) > (tf + fabsf(tf) * 1e-6f));  // NaN -> visit
+}
+
+// Cube-map cell of a direction (hrt_bvh.cpp face_dir is the inverse): face = 2 * major axis +
+// (component < 0), (u, v) = the two minor components over the major one's magnitude.
+__device__ __forceinline__ uint32_t dir_cell(f3 d) {
+  const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+  uint32_t face;
+  float u, v;
+  if (ax >= ay && ax >= az) {
+    face = d.x < 0.0f ? 1u : 0u;
+    u = d.y / ax;
+    v = d.z / ax;
+  } else if (ay >= az) {
+    face = d.y < 0.0f ? 3u : 2u;
+    u = d.z / ay;
+    v = d.x / ay;
+  } else {
+    face = d.z < 0.0f ? 5u : 4u;
+    u = d.x / az;
+    v = d.y / az;
+  }
+  const float s = 0.5f * (float)kDirRes;
+  const int iu = min(kDirRes - 1, max(0, (int)((u + 1.0f) * s)));  // NaN converts to 0
+  const int iv = min(kDirRes - 1, max(0, (int)((v + 1.0f) * s)));
+  return (face * kDirRes + (uint32_t)iu) * kDirRes + (uint32_t)iv;
+}
+
+// Bounce segments through the hierarchy.  Called with ALL 64 lanes active (spheres and the
+// irregular list are wave-uniform loops; the traversal and the band list are per lane).
+__device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const TraceParams& P, bool sec, f3 o, f3 d,
+                                                     uint32_t& tests, Closest& c, Diag& dg) {
+  const hrt_push_constants& pc = P.pc;
+  spheres_first(sc, pc, sec, o, d, c);
+  unsigned long long mask = 0ull;
+  if (sec) {
+    for (int m = 0; m < pc.num_meshes; ++m) {
+      const hrt_mesh& mesh = sc.meshes[m];
+      if (aabb_pass(mesh, o, d)) {
+        mask |= 1ull << m;
+        tests += mesh.len;
+      }
+    }
+  }
+  uint32_t bkey = 0;  // spheres (and "no hit") win every tie
+  float best_k = c.t * kOnePlus;
+  for (uint32_t k = 0; k < P.bvh_n_irregular; ++k)
+    if (sec) bvh_prim_test(P.bvh_irregular, k, mask, o, d, c, bkey, best_k);
+  const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const float4* __restrict__ nodes = P.bvh_nodes;
+  const uint32_t end = P.bvh_n_nodes;
+  uint32_t node = (sec && mask) ? 0u : end;
+  uint32_t visits = 0, prim_tests = 0, band_tests = 0;
+  if (sec && mask) {
+    const uint32_t cell = dir_cell(d);
+    const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
+    // Pre-check: the stored n^ is within 1e-7 of n / |n| per component, so |d.n^stored - d.n^| < 1e-6
+    // and an entry outside (-kBandTau - 2e-5, 3e-5) is not in this lane's band.
+    const float lo = -kBandTau - 2e-5f, hi = 3e-5f;
+    uint32_t k = b0;
+    for (; k + 4 <= b1; k += 4) {
+      const float4 q0 = P.bvh_band[k], q1 = P.bvh_band[k + 1], q2 = P.bvh_band[k + 2], q3 = P.bvh_band[k + 3];
+      const float4 qs[4] = {q0, q1, q2, q3};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float dn = d.x * qs[j].x + d.y * qs[j].y + d.z * qs[j].z;
+        if (dn > lo && dn < hi) {
+          bvh_prim_test(P.bvh_prims, __builtin_bit_cast(uint32_t, qs[j].w), mask, o, d, c, bkey, best_k);
+          ++band_tests;
+        }
+      }
+    }
+    for (; k < b1; ++k) {
+      const float4 q = P.bvh_band[k];
+      const float dn = d.x * q.x + d.y * q.y + d.z * q.z;
+      if (dn > lo && dn < hi) {
+        bvh_prim_test(P.bvh_prims, __builtin_bit_cast(uint32_t, q.w), mask, o, d, c, bkey, best_k);
+        ++band_tests;
+      }
+    }
+  }
+  while (node < end) {
+    const float4 N0 = nodes[4 * node], N1 = nodes[4 * node + 1], N2 = nodes[4 * node + 2], N3 = nodes[4 * node + 3];
+    const uint32_t info = __builtin_bit_cast(uint32_t, N3.z);
+    const uint32_t esc = __builtin_bit_cast(uint32_t, N3.w);
+    const bool visit = bvh_node_visit(N0, N1, N2, N3, o, d, inv, c.t);
+    const uint32_t count = info >> 27;
+    ++visits;
+    if (visit && count) {
+      const uint32_t first = info & 0x07FFFFFFu;
+      for (uint32_t k = first; k < first + count; ++k) bvh_prim_test(P.bvh_prims, k, mask, o, d, c, bkey, best_k);
+      prim_tests += count;
+    }
+    node = (visit && !count) ? node + 1 : esc;
+  }
+  if (P.diag) {
+    dg.bvh_visits += visits;
+    dg.bvh_prims += prim_tests;
+    dg.bvh_band += band_tests;
+  }
+}
+
+// Fused loop of BUNDLE / BUNDLE_CULL / BUNDLE_BVH.  Every lane stays in the loop until the whole wave is done, so
 // the loop top is a full-wave region (lane-parallel culls and shuffles need all 64 lanes).  Primary
 // segments take the bundle path; a lane whose next segment is a bounce waits (state untouched) until
 // at least sec_batch lanes wait or no primary segment is left in the wave, then all waiting lanes run
 // their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
-template <bool BounceCull>
+enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2 };
+
+template <int Bounce>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
@@ -689,19 +878,25 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     const bool run_sec = nwait > 0 && (nwait >= P.sec_batch || !any_prim);
     const bool sec = waiting && run_sec;
     Closest c{kFltMax, 0, 0u, 0u};
+    uint64_t t0 = 0, t1 = 0, t2 = 0;
     if (P.diag) {
       dg.prim_iters += any_prim ? 1u : 0u;
       dg.sec_iters += run_sec ? 1u : 0u;
       dg.sec_lanes += run_sec ? nwait : 0u;
+      t0 = __builtin_readcyclecounter();
     }
     if (any_prim) world_hit_bundle(sc, P, prim, p.pos, p.dir, tests, c, dg);
+    if (P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
-      if constexpr (BounceCull) {
+      if constexpr (Bounce == kBounceBvh) {
+        world_hit_bounce_bvh(sc, P, sec, p.pos, p.dir, tests, c, dg);
+      } else if constexpr (Bounce == kBounceCull) {
         world_hit_bounce_cull(sc, P, sec, p.pos, p.dir, tests, c, dg);
       } else {
         if (sec) c = world_hit_brute(sc, src, pc, p.pos, p.dir, tests);
       }
     }
+    if (P.diag) t2 = __builtin_readcyclecounter();
     if (prim || sec) {
       ++segs;
       const bool ended = shade_step(sc, pc, p, c, state);
@@ -711,6 +906,12 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
         p.bounce = pc.max_bounces + 1;
       }
     }
+    if (P.diag) {
+      const uint64_t t3 = __builtin_readcyclecounter();
+      dg.cyc_prim += t1 - t0;
+      dg.cyc_sec += t2 - t1;
+      dg.cyc_shade += t3 - t2;
+    }
   }
   if (active) {
     colour = colour / (float)pc.num_samples;
@@ -718,6 +919,9 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   }
   flush_counters(P, segs, tests);
   if (P.diag && (threadIdx.x & 63) == 0) {
+    atomicAdd(&P.diag[10], (unsigned long long)dg.cyc_prim);
+    atomicAdd(&P.diag[11], (unsigned long long)dg.cyc_sec);
+    atomicAdd(&P.diag[12], (unsigned long long)dg.cyc_shade);
     atomicAdd(&P.diag[0], (unsigned long long)dg.prim_iters);
     atomicAdd(&P.diag[1], (unsigned long long)dg.prim_considered);
     atomicAdd(&P.diag[2], (unsigned long long)dg.prim_survivors);
@@ -726,18 +930,33 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[5], (unsigned long long)dg.sec_survivors);
     atomicAdd(&P.diag[6], (unsigned long long)dg.sec_lanes);
   }
+  if (P.diag && Bounce == kBounceBvh) {
+    atomicAdd(&P.diag[7], (unsigned long long)dg.bvh_visits);
+    atomicAdd(&P.diag[8], (unsigned long long)dg.bvh_prims);
+    atomicAdd(&P.diag[9], (unsigned long long)dg.bvh_band);
+  }
 }
 
 __global__ __launch_bounds__(256) void trace_bundle(TraceParams P) {
   uint32_t x, lr;
   lane_pixel(P, x, lr);
-  trace_fused_split<false>(P, x, lr);
+  trace_fused_split<kBounceBrute>(P, x, lr);
 }
 
-__global__ __launch_bounds__(256) void trace_bundle_cull(TraceParams P) {
+#ifndef HRT_CULL_WAVES
+#define HRT_CULL_WAVES 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HRT_CULL_WAVES))) void trace_bundle_cull(
+    TraceParams P) {
   uint32_t x, lr;
   lane_pixel(P, x, lr);
-  trace_fused_split<true>(P, x, lr);
+  trace_fused_split<kBounceCull>(P, x, lr);
+}
+
+__global__ __launch_bounds__(256) void trace_bundle_bvh(TraceParams P) {
+  uint32_t x, lr;
+  lane_pixel(P, x, lr);
+  trace_fused_split<kBounceBvh>(P, x, lr);
 }
 
 // Per-frame prep for the bundle variants: one workgroup per mesh, order-preserving compaction of the
@@ -863,12 +1082,17 @@ namespace hrt {
 
 static inline unsigned blocks_for(size_t n) { return (unsigned)((n + 255) / 256); }
 constexpr size_t kMaxLdsScene = 160 * 1024;
-constexpr uint32_t kAutoCullTris = 256;  // BUNDLE_CULL from this many mesh triangles, BUNDLE below
+constexpr uint32_t kAutoCullTris = 256;   // BUNDLE_CULL from this many mesh triangles, BUNDLE below
+constexpr uint32_t kAutoBvhTris = 4096;   // BUNDLE_BVH from this many (profiles/r01d_bvh_scaling.log)
 
 int resolve_variant(const TraceParams& p, int variant) {
-  if (variant == HRT_KERNEL_AUTO) variant = p.cam_list_capacity >= kAutoCullTris ? HRT_KERNEL_BUNDLE_CULL
-                                                                                 : HRT_KERNEL_BUNDLE;
+  if (variant == HRT_KERNEL_AUTO) {
+    variant = p.cam_list_capacity >= kAutoBvhTris && p.bvh_nodes ? HRT_KERNEL_BUNDLE_BVH
+              : p.cam_list_capacity >= kAutoCullTris             ? HRT_KERNEL_BUNDLE_CULL
+                                                                 : HRT_KERNEL_BUNDLE;
+  }
   if (variant == HRT_KERNEL_BRUTE_LDS && (size_t)p.n_tris * 48 > kMaxLdsScene) variant = HRT_KERNEL_BRUTE;
+  if (variant == HRT_KERNEL_BUNDLE_BVH && (!p.bvh_nodes || p.pc.num_meshes > 64)) variant = HRT_KERNEL_BUNDLE_CULL;
   if (p.pc.max_bounces < 0) variant = HRT_KERNEL_LITERAL;  // the fused loops assume >= 1 segment per path
   return variant;
 }
@@ -893,11 +1117,14 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream) {
     }
     case HRT_KERNEL_BUNDLE:
     case HRT_KERNEL_BUNDLE_CULL:
+    case HRT_KERNEL_BUNDLE_BVH:
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       if (variant == HRT_KERNEL_BUNDLE)
         trace_bundle<<<grid, 256, 0, stream>>>(p);
-      else
+      else if (variant == HRT_KERNEL_BUNDLE_CULL)
         trace_bundle_cull<<<grid, 256, 0, stream>>>(p);
+      else
+        trace_bundle_bvh<<<grid, 256, 0, stream>>>(p);
       break;
     default:
       trace_brute<<<grid, 256, 0, stream>>>(p);

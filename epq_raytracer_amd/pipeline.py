@@ -151,6 +151,12 @@ class HrtContext:
         self._check(self.lib.hrt_get_diagnostics(self.handle, _lib.ptr(out), len(out)), "hrt_get_diagnostics")
         return dict(zip(_lib.DIAG_NAMES, (int(v) for v in out)))
 
+    def scene_info(self) -> dict:
+        """What the last set_scene built for the BVH kernel (hrt_get_scene_info)."""
+        out = np.zeros(len(_lib.SCENE_INFO_NAMES), np.uint32)
+        self._check(self.lib.hrt_get_scene_info(self.handle, _lib.ptr(out), len(out)), "hrt_get_scene_info")
+        return dict(zip(_lib.SCENE_INFO_NAMES, (int(v) for v in out)))
+
     def reset_stats(self):
         self._check(self.lib.hrt_reset_stats(self.handle), "hrt_reset_stats")
 

@@ -110,6 +110,27 @@ class Mesh:
             raise ValueError("mesh index count must be a multiple of 3")
 
 
+def subdivide(mesh: Mesh, k: int) -> Mesh:
+    """Split every triangle (a, b, c) into k*k triangles on the same plane, same winding (a scaling
+    workload: the same surface with k*k times the triangles; not a reference feature)."""
+    if k <= 1:
+        return mesh
+    tri = mesh.positions[mesh.indices.reshape(-1, 3)].astype(np.float64)  # (T, 3, 3)
+    a, ab, ac = tri[:, 0], tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0]
+    grid = [(i, j) for i in range(k + 1) for j in range(k + 1 - i)]
+    gid = {g: n for n, g in enumerate(grid)}
+    pts = np.stack([a + ab * (i / k) + ac * (j / k) for i, j in grid], 1)  # (T, G, 3)
+    local = []
+    for i in range(k):
+        for j in range(k - i):
+            local.append((gid[(i, j)], gid[(i + 1, j)], gid[(i, j + 1)]))
+            if i + j + 1 < k:
+                local.append((gid[(i + 1, j)], gid[(i + 1, j + 1)], gid[(i, j + 1)]))
+    local = np.array(local, np.uint32)
+    base = (np.arange(len(tri), dtype=np.uint32) * len(grid))[:, None, None]
+    return Mesh(pts.reshape(-1, 3).astype(np.float32), (base + local[None]).reshape(-1), mesh.name)
+
+
 @dataclass
 class Sphere:
     """src/objects.rs:8-22."""

@@ -11,7 +11,7 @@ import numpy as np
 from .app import RayTracingApp
 from .pipeline import RayTracerSettings
 from .scene import (Camera, CustomMaterial, InvisLightMaterial, LambertianMaterial, LightMaterial, MetalMaterial,
-                    RayTracingMesh, Sphere, load_asset)
+                    RayTracingMesh, Sphere, load_asset, subdivide)
 
 F = np.float32
 
@@ -112,8 +112,25 @@ PRESETS = {
 }
 
 
-def make_app(name: str, num_samples=None, max_bounces=None, **kw) -> RayTracingApp:
+def scaled_preset(name: str, k: int):
+    """Preset `name` with every mesh triangle split into k*k (scene.subdivide): the triangle-count
+    scaling workload for the kernel variants (e.g. "island@4" = 16x the island's triangles)."""
     cam, settings = PRESETS[name]()
+    for rm in settings.mesh_data:
+        rm.mesh = subdivide(rm.mesh, k)
+    return cam, settings
+
+
+def preset(name: str):
+    """PRESETS[name]() or, for "<preset>@<k>", scaled_preset(preset, k)."""
+    if "@" in name:
+        base, k = name.split("@")
+        return scaled_preset(base, int(k))
+    return PRESETS[name]()
+
+
+def make_app(name: str, num_samples=None, max_bounces=None, **kw) -> RayTracingApp:
+    cam, settings = preset(name)
     if num_samples is not None:
         settings.num_samples = num_samples
     if max_bounces is not None:

@@ -150,12 +150,15 @@ typedef struct hrt_context hrt_context;
 /* Trace kernel variants (HRT_OPT_KERNEL_VARIANT).  All produce byte-identical frames and counters;
  * they differ only in how much of the reference's brute-force work they prove unnecessary. */
 typedef enum hrt_kernel {
-  HRT_KERNEL_AUTO = 0,        /* BUNDLE_CULL for scenes with >= 256 mesh triangles, BUNDLE below */
+  HRT_KERNEL_AUTO = 0,        /* BUNDLE below 256 mesh triangles, BUNDLE_CULL below 4096, BUNDLE_BVH above */
   HRT_KERNEL_LITERAL = 1,     /* raytracing.glsl's loop shape, the full test on every triangle */
   HRT_KERNEL_BRUTE = 2,       /* fused sample/bounce loop, two-stage exact pre-test, triangles via SGPRs */
   HRT_KERNEL_BRUTE_LDS = 3,   /* BRUTE with the scene resident in LDS (falls back to BRUTE above 160 KiB) */
   HRT_KERNEL_BUNDLE = 4,      /* primary rays: lane-parallel bundle cull; bounces: deferred, BRUTE test */
-  HRT_KERNEL_BUNDLE_CULL = 5  /* BUNDLE + lane-parallel origin-box / direction-cone cull of bounce rays */
+  HRT_KERNEL_BUNDLE_CULL = 5, /* BUNDLE + lane-parallel origin-box / direction-cone cull of bounce rays */
+  HRT_KERNEL_BUNDLE_BVH = 6   /* BUNDLE + per-lane BVH traversal of bounce rays (hierarchy built by
+                                 hrt_set_scene; falls back to BUNDLE_CULL above 64 meshes or 2^18
+                                 mesh triangles) */
 } hrt_kernel;
 
 /* Option keys for hrt_set_option. */
@@ -167,7 +170,9 @@ typedef enum hrt_option {
   HRT_OPT_COUNTERS = 2,
   /* bundle kernel: a wave runs its bounce (non-primary) segments once this many lanes wait for one,
    * or when no lane has a primary segment left (1..64, default 48; results do not depend on it) */
-  HRT_OPT_SECONDARY_BATCH = 3
+  HRT_OPT_SECONDARY_BATCH = 3,
+  /* BUNDLE_BVH: triangles per leaf of the hierarchy the next hrt_set_scene builds (1..16, default 4) */
+  HRT_OPT_BVH_LEAF_SIZE = 4
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */
@@ -179,8 +184,26 @@ typedef enum hrt_diag {
   HRT_DIAG_BOUNCE_CONSIDERED = 4,  /* triangles bounded by the bounce pre-cull (per wave) */
   HRT_DIAG_BOUNCE_SURVIVORS = 5,   /* ... of which survived */
   HRT_DIAG_BOUNCE_LANES = 6,       /* lanes in bounce batches */
-  HRT_NUM_DIAG = 7
+  HRT_DIAG_BVH_VISITS = 7,         /* BUNDLE_BVH: node visits summed over bounce lanes */
+  HRT_DIAG_BVH_PRIM_TESTS = 8,     /* BUNDLE_BVH: leaf triangles reached, summed over bounce lanes */
+  HRT_DIAG_BVH_BAND_TESTS = 9,     /* BUNDLE_BVH: grazing-band triangles tested, summed over bounce lanes */
+  HRT_DIAG_PRIMARY_CYCLES = 10,    /* shader clocks per wave in the primary cull + tests, summed */
+  HRT_DIAG_BOUNCE_CYCLES = 11,     /* ... in the bounce-batch path */
+  HRT_DIAG_SHADE_CYCLES = 12,      /* ... in shading (scatter, RNG, colour) */
+  HRT_NUM_DIAG = 13
 } hrt_diag;
+
+/* What hrt_set_scene built for BUNDLE_BVH (hrt_get_scene_info). */
+typedef enum hrt_scene_info {
+  HRT_SCENE_BVH_NODES = 0,      /* hierarchy nodes */
+  HRT_SCENE_BVH_PRIMS = 1,      /* (mesh, triangle) entries in its leaves */
+  HRT_SCENE_BVH_IRREGULAR = 2,  /* entries outside the cull analysis (non-finite, normal != e1 x e2, ...):
+                                   tested against every bounce ray */
+  HRT_SCENE_BVH_NEVER = 3,      /* entries with a zero normal, which the reference never accepts */
+  HRT_SCENE_BVH_BUILT = 4,      /* 1 if built (0: > 64 meshes or > 2^18 entries -> BUNDLE_BVH runs BUNDLE_CULL) */
+  HRT_SCENE_BVH_BAND_ENTRIES = 5, /* grazing-band list entries over all direction cells */
+  HRT_NUM_SCENE_INFO = 6
+} hrt_scene_info;
 
 uint32_t hrt_abi_version(void);
 
@@ -210,6 +233,9 @@ hrt_status hrt_synchronize(hrt_context* ctx);
 hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out); /* synchronizes */
 hrt_status hrt_reset_stats(hrt_context* ctx);
 hrt_status hrt_get_diagnostics(hrt_context* ctx, uint64_t* out, uint32_t count); /* synchronizes */
+/* Extension (no reference counterpart): out[i] = hrt_scene_info i for i < count, from the last
+ * hrt_set_scene. */
+hrt_status hrt_get_scene_info(hrt_context* ctx, uint32_t* out, uint32_t count);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
 /* HIP stream the context's work is ordered on (hipStream_t), for callers that interoperate. */

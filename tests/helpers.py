@@ -21,7 +21,7 @@ class SceneCase:
     def __init__(self, name=None, size=(64, 64), num_samples=1, max_bounces=1, rng_offset=1, settings=None,
                  camera=None):
         if settings is None:
-            camera, settings = E.PRESETS[name]()
+            camera, settings = E.preset(name)
         settings.num_samples, settings.max_bounces = num_samples, max_bounces
         self.name, self.size, self.camera, self.settings = name, tuple(size), camera, settings
         self.rays, self.n_rays, jit = E.create_rays(size, settings.camera_focal_length, settings.viewport_height,
@@ -54,10 +54,13 @@ class SceneCase:
         return pyoracle.trace(self.push(rng_offset), self.rays, self.spheres, self.tris, self.meshes, rows=rows,
                               nthreads=nthreads, want_f32=want_f32)
 
-    def context(self, mode=_lib.MODE_RGBA8, partition=None, variant=0, device=0):
+    def context(self, mode=_lib.MODE_RGBA8, partition=None, variant=0, device=0, options=None):
+        """options: {hrt_option: value} applied before set_scene (e.g. the BVH leaf size)."""
         ctx = E.HrtContext(self.size, device=device, mode=mode, partition=partition)
-        ctx.set_scene(self.rays, self.spheres, self.tris, self.meshes)
         ctx.set_option(_lib.OPT_KERNEL_VARIANT, variant)
+        for k, v in (options or {}).items():
+            ctx.set_option(k, v)
+        ctx.set_scene(self.rays, self.spheres, self.tris, self.meshes)
         return ctx
 
     def gpu(self, rng_offset=None, mode=_lib.MODE_RGBA8, variant=0, fmt=None):

@@ -14,7 +14,7 @@ from helpers import E, SceneCase, _lib, mismatch_report
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [0, 1]  # auto (tuned), literal
-ALL_VARIANTS = list(range(6))  # every hrt_kernel value  # every kernel variant (hrt_set_option HRT_OPT_KERNEL_VARIANT)
+ALL_VARIANTS = list(range(7))  # every hrt_kernel value (hrt_set_option HRT_OPT_KERNEL_VARIANT)
 
 CONFIGS = [
     # (scene, size, spp, bounces, rng_offset)
@@ -217,6 +217,99 @@ def test_degenerate_and_adversarial_geometry():
         assert (gseg, gtt) == (seg, tt)
 
 
+def _grid_terrain(n=24, size=8.0, bumps=40, seed=3):
+    """n x n quads on the y = 0 plane (two triangles each), some vertices lifted: large coplanar
+    regions (grazing bounce rays, the BVH cull's ill-conditioned case) next to tilted facets."""
+    rng = np.random.default_rng(seed)
+    xs = np.linspace(-size, size, n + 1, dtype=np.float32)
+    gx, gz = np.meshgrid(xs, xs, indexing="ij")
+    gy = np.zeros_like(gx)
+    for _ in range(bumps):
+        i, j = rng.integers(1, n, size=2)
+        gy[i, j] = rng.uniform(-0.3, 0.6)
+    v = np.stack([gx, gy, gz], -1).reshape(-1, 3).astype(np.float32)
+    idx = []
+    for i in range(n):
+        for j in range(n):
+            a, b, c, d = i * (n + 1) + j, (i + 1) * (n + 1) + j, i * (n + 1) + j + 1, (i + 1) * (n + 1) + j + 1
+            idx += [a, c, b, b, c, d]
+    return E.Mesh(v, np.array(idx, np.uint32))
+
+
+@pytest.mark.parametrize("eye_y", [0.0, 0.01, 1.5])
+def test_grazing_coplanar_terrain(eye_y):
+    """Coplanar floor triangles seen and bounced at grazing angles, the camera ON the floor plane
+    (eye_y = 0), rough metal (fuzzed reflections near the plane): every variant, including the
+    BVH's per-lane cull, must agree with the oracle byte for byte."""
+    terrain = _grid_terrain()
+    st = E.RayTracerSettings(num_samples=3, max_bounces=8, use_environment_lighting=True,
+                             sphere_data=[E.Sphere([0.0, 0.5, 0.0], 0.5, E.LambertianMaterial([0.9, 0.3, 0.3]))],
+                             mesh_data=[E.RayTracingMesh(terrain, E.MetalMaterial([0.8, 0.8, 0.7], 0.9, 0.4)),
+                                        E.RayTracingMesh(_grid_terrain(6, 2.0, 5, 9),
+                                                         E.LambertianMaterial([0.3, 0.6, 0.3]))])
+    cam = E.Camera([-7.5, eye_y, -0.3], [1.0, -0.02 if eye_y > 0 else 0.0, 0.05])
+    case = SceneCase(settings=st, camera=cam, size=(96, 64), num_samples=3, max_bounces=8)
+    ref, _, seg, tt = case.oracle()
+    for variant in ALL_VARIANTS:
+        img, gseg, gtt = case.gpu(variant=variant)
+        assert np.array_equal(img, ref), f"variant {variant}: " + mismatch_report(img, ref)
+        assert (gseg, gtt) == (seg, tt)
+
+
+def test_bvh_scene_info_and_mesh_limit():
+    """hrt_set_scene builds the BVH over every (mesh, triangle) entry; above 64 meshes it is not
+    built and BUNDLE_BVH runs BUNDLE_CULL (same bytes either way)."""
+    case = SceneCase("island", (64, 48), 2, 6)
+    ctx = case.context()
+    info = ctx.scene_info()
+    ctx.close()
+    assert info["bvh_built"] == 1
+    assert info["bvh_prims"] + info["bvh_irregular"] + info["bvh_never"] == sum(int(m["len"]) for m in case.meshes)
+    assert info["bvh_prims"] > 0 and info["bvh_nodes"] >= 1
+    rng = np.random.default_rng(5)
+    meshes = []
+    for k in range(70):
+        c = rng.uniform(-4, 4, 3)
+        v = (c + rng.uniform(-1, 1, (3, 3))).astype(np.float32)
+        meshes.append(E.RayTracingMesh(E.Mesh(v, np.arange(3, dtype=np.uint32)),
+                                       E.LambertianMaterial(list(rng.uniform(0.2, 0.9, 3)))))
+    st = E.RayTracerSettings(num_samples=2, max_bounces=5, use_environment_lighting=True, mesh_data=meshes)
+    case = SceneCase(settings=st, camera=E.Camera([0.0, 0.0, -12.0], [0.0, 0.0, 1.0]), size=(48, 40),
+                     num_samples=2, max_bounces=5)
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context()
+    assert ctx.scene_info()["bvh_built"] == 0
+    ctx.close()
+    for variant in (_lib.KERNEL_BUNDLE_CULL, _lib.KERNEL_BUNDLE_BVH):
+        img, gseg, gtt = case.gpu(variant=variant)
+        assert np.array_equal(img, ref) and (gseg, gtt) == (seg, tt)
+
+
+def test_large_scene_auto_picks_bvh():
+    """island@2 (6.4K triangles, every island triangle split in four): AUTO runs BUNDLE_BVH
+    (>= 4096 mesh triangles) and matches the oracle and BUNDLE_CULL byte for byte."""
+    case = SceneCase("island@2", (96, 64), 2, 8)
+    assert sum(int(m["len"]) for m in case.meshes) >= 4096
+    ref, _, seg, tt = case.oracle()
+    for variant in (_lib.KERNEL_AUTO, _lib.KERNEL_BUNDLE_CULL, _lib.KERNEL_BUNDLE_BVH):
+        img, gseg, gtt = case.gpu(variant=variant)
+        assert np.array_equal(img, ref), f"variant {variant}: " + mismatch_report(img, ref)
+        assert (gseg, gtt) == (seg, tt)
+
+
+@pytest.mark.parametrize("leaf", [1, 2, 8, 16])
+def test_bvh_leaf_sizes(leaf):
+    case = SceneCase("cave", (80, 48), 2, 8)
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context(options={_lib.OPT_BVH_LEAF_SIZE: leaf, _lib.OPT_KERNEL_VARIANT: _lib.KERNEL_BUNDLE_BVH})
+    ctx.trace(case.push())
+    img = ctx.read(_lib.IMG_TRACE)
+    s = ctx.stats()
+    ctx.close()
+    assert np.array_equal(img, ref), mismatch_report(img, ref)
+    assert (s.segments, s.tri_tests) == (seg, tt)
+
+
 def test_errors_fail_loudly():
     case = SceneCase("box", (32, 32), 1, 1)
     ctx = E.HrtContext((32, 32), device=0)
@@ -253,11 +346,14 @@ def headline():
     img1b = ctx.read(_lib.IMG_TRACE)
     ctx.trace(case.push(2))
     img2 = ctx.read(_lib.IMG_TRACE)
-    ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
-    ctx.trace(case.push(1))
-    lit = ctx.read(_lib.IMG_TRACE)
+    others = {}
+    for v in (_lib.KERNEL_BUNDLE_CULL, _lib.KERNEL_BUNDLE_BVH, _lib.KERNEL_LITERAL):
+        ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
+        ctx.reset_stats()
+        ctx.trace(case.push(1))
+        others[v] = (ctx.read(_lib.IMG_TRACE), ctx.stats())
     ctx.close()
-    return case, img1, img1b, img2, lit, st
+    return case, img1, img1b, img2, others, st
 
 
 def test_headline_rows_bit_exact(headline):
@@ -269,10 +365,12 @@ def test_headline_rows_bit_exact(headline):
 
 
 def test_headline_properties(headline):
-    case, img1, img1b, img2, lit, st = headline
+    case, img1, img1b, img2, others, st = headline
     assert np.array_equal(img1, img1b)           # deterministic
     assert not np.array_equal(img1, img2)        # rng_offset changes the frame
-    assert np.array_equal(img1, lit)             # tuned == literal at full size
+    for v, (img, s) in others.items():           # every tuned variant == literal at full size
+        assert np.array_equal(img1, img), _lib.KERNEL_NAMES[v]
+        assert (s.segments, s.tri_tests) == (st.segments, st.tri_tests), _lib.KERNEL_NAMES[v]
     assert (img1[..., 3] == 255).all()
     n = 1920 * 1080 * 64
     assert n <= st.segments <= 9 * n             # every path: 1..max_bounces+1 segments

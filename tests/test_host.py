@@ -170,3 +170,22 @@ def test_presets_build_records():
     assert [len(m.mesh.indices) // 3 for m in st.mesh_data] == [80, 992, 180, 358]
     cam, st = E.load_box_scene()
     assert st.mesh_data[-1].material.into()["settings"][3] == 1.0   # invisible light flag
+
+
+def test_subdivide_preserves_surface_and_winding():
+    """scene.subdivide (the triangle-count scaling workload): k*k triangles per input triangle,
+    same total area, every piece's normal parallel to (and oriented like) its parent's."""
+    import epq_raytracer_amd as E
+    rng = np.random.default_rng(2)
+    v = rng.uniform(-3, 3, (12, 3)).astype(np.float32)
+    m = E.Mesh(v, np.arange(12, dtype=np.uint32))
+    for k in (1, 2, 3, 5):
+        s = E.subdivide(m, k)
+        assert len(s.indices) == 3 * 4 * k * k
+        p = s.positions[s.indices.reshape(-1, 3)].astype(np.float64)
+        q = m.positions[m.indices.reshape(-1, 3)].astype(np.float64)
+        ns = np.cross(p[:, 1] - p[:, 0], p[:, 2] - p[:, 0]).reshape(4, k * k, 3)
+        nq = np.cross(q[:, 1] - q[:, 0], q[:, 2] - q[:, 0])
+        np.testing.assert_allclose(np.linalg.norm(ns, axis=-1).sum(1), np.linalg.norm(nq, axis=-1), rtol=1e-4)
+        cos = np.einsum("tkc,tc->tk", ns, nq) / (np.linalg.norm(ns, axis=-1) * np.linalg.norm(nq, axis=-1)[:, None])
+        assert (cos > 0.9999).all()

@@ -31,10 +31,12 @@ def main():
     ap.add_argument("--no-ref", action="store_true", help="skip the literal-kernel reference frame")
     ap.add_argument("--diag", action="store_true", help="also print the bundle kernels' cull diagnostics")
     ap.add_argument("--sec-batch", type=int, nargs="+", default=[48], help="HRT_OPT_SECONDARY_BATCH values to sweep")
+    ap.add_argument("--leaf", type=int, default=None, help="HRT_OPT_BVH_LEAF_SIZE for the scene build")
     a = ap.parse_args()
     W, H = (int(v) for v in a.size.split("x"))
     case = SceneCase(a.scene, (W, H), a.spp, a.bounces)
-    ctx = case.context()
+    ctx = case.context(options={_lib.OPT_BVH_LEAF_SIZE: a.leaf} if a.leaf else None)
+    print(json.dumps({"scene_info": ctx.scene_info()}), flush=True)
     pc = case.push(1)
     # warm up + reference image (literal kernel), unless profiling one variant alone
     ref = None
@@ -42,7 +44,7 @@ def main():
         ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
         ctx.trace(pc)
         ref = ctx.read(_lib.IMG_TRACE)
-    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v in (0, 4, 5) else [a.sec_batch[0]])]
+    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v in (0, 4, 5, 6) else [a.sec_batch[0]])]
     res = {vs: [] for vs in combos}
     stats = {}
     same = {}
@@ -59,7 +61,7 @@ def main():
                 same[(v, sb)] = None if ref is None else bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
     if a.diag:
         for v in a.variants:
-            if v in (0, 4, 5):
+            if v in (0, 4, 5, 6):
                 ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
                 ctx.set_option(_lib.OPT_COUNTERS, 2)
                 ctx.reset_stats()
@@ -69,6 +71,14 @@ def main():
                 d["primary_survival"] = d["primary_survivors"] / max(d["primary_considered"], 1)
                 d["bounce_survival"] = d["bounce_survivors"] / max(d["bounce_considered"], 1)
                 d["bounce_lanes_per_iter"] = d["bounce_lanes"] / max(d["bounce_iters"], 1)
+                d["bvh_visits_per_lane"] = d["bvh_visits"] / max(d["bounce_lanes"], 1)
+                d["bvh_prims_per_lane"] = d["bvh_prim_tests"] / max(d["bounce_lanes"], 1)
+                d["bvh_band_per_lane"] = d["bvh_band_tests"] / max(d["bounce_lanes"], 1)
+                cyc = d["primary_cycles"] + d["bounce_cycles"] + d["shade_cycles"]
+                for ph in ("primary", "bounce", "shade"):
+                    d[ph + "_cycle_share"] = d[ph + "_cycles"] / max(cyc, 1)
+                d["bounce_cycles_per_iter"] = d["bounce_cycles"] / max(d["bounce_iters"], 1)
+                d["primary_cycles_per_iter"] = d["primary_cycles"] / max(d["primary_iters"], 1)
                 print(json.dumps(d), flush=True)
                 ctx.set_option(_lib.OPT_COUNTERS, 1)
     out = []
