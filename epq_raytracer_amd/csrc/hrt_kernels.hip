@@ -527,11 +527,21 @@ __device__ __forceinline__ void spheres_first(const Scene& sc, const hrt_push_co
   }
 }
 
+// Read-only scene data seen through the constant address space: a load with a wave-uniform address
+// from it is a scalar (s_load) load.
+typedef __attribute__((address_space(4))) const float kfloat;
+__device__ __forceinline__ const kfloat* to_const(const float4* p) {
+  return (const kfloat*)(const __attribute__((address_space(4))) void*)(p);
+}
+__device__ __forceinline__ float4 ldk(const kfloat* p, uint32_t i) {  // float4 i of p
+  return make_float4(p[4 * i], p[4 * i + 1], p[4 * i + 2], p[4 * i + 3]);
+}
+
 // Exact per-lane test of compacted camera-facing record k (ao and num_t precomputed), entered only
 // when some lane has dn < 0.
-__device__ __forceinline__ void primary_exact(const float4* __restrict__ ct, uint32_t k, float dn, f3 d, uint32_t m,
-                                              Closest& c, float& best_k) {
-  const float4 A = ct[4 * k], B = ct[4 * k + 1], C = ct[4 * k + 2];
+__device__ __forceinline__ void primary_exact(const kfloat* ct, uint32_t k, float dn, f3 d, uint32_t m, Closest& c,
+                                              float& best_k) {
+  const float4 A = ldk(ct, 4 * k), B = ldk(ct, 4 * k + 1), C = ldk(ct, 4 * k + 2);
   TriPre q;
   q.num_t = A.w;
   const f3 dao = cross(mk(A.x, A.y, A.z), d);
@@ -544,6 +554,110 @@ __device__ __forceinline__ void primary_exact(const float4* __restrict__ ct, uin
   }
 }
 
+// ---- per-wave primary triangle list ------------------------------------------------------------
+// Every primary direction a wave can produce is normalize(M * nc) with nc = centre + (0, t2.y, t1.z),
+// |t1.z|, |t2.y| <= jitter_size (get_ray_dir, raytracing.glsl:162-166), i.e. nc in the box X =
+// [centre box of the wave's pixels] + [0] x [-j, j] x [-j, j].  The cap around normalize(M * mid(X))
+// through the farthest of X's 8 corner directions contains them all (a cap under 90 degrees is
+// convex), widened by 1e-5 in cosine for rounding.  The bundle cull against that cap runs ONCE per
+// wave; its survivors (camera-list index | mesh << 27, in buffer order) are the only triangles any
+// primary segment of the wave can hit, so each primary iteration tests just those.
+constexpr uint32_t kTileCap = 256;  // list entries per wave (LDS); more -> per-iteration cull
+
+struct TileList {
+  const uint32_t* e;  // this wave's slice of the block's LDS list
+  uint32_t n;
+  bool ok;
+};
+
+__device__ __forceinline__ Bundle tile_bundle(const hrt_push_constants& pc, bool active, f3 centre, bool& ok) {
+  const float inf = __builtin_inff();
+  const f3 lo = mk(wave_min_all(active ? centre.x : inf), wave_min_all(active ? centre.y : inf),
+                   wave_min_all(active ? centre.z : inf));
+  const f3 hi = mk(wave_max_all(active ? centre.x : -inf), wave_max_all(active ? centre.y : -inf),
+                   wave_max_all(active ? centre.z : -inf));
+  const float j = fabsf(pc.jitter_size) * 1.0001f;
+  const float* M = pc.cam_alignment_mat;
+  auto dir = [&](f3 v) {
+    return normalize(mk(M[0] * v.x + M[4] * v.y + M[8] * v.z, M[1] * v.x + M[5] * v.y + M[9] * v.z,
+                        M[2] * v.x + M[6] * v.y + M[10] * v.z));
+  };
+  Bundle b;
+  b.a = dir(mk(0.5f * lo.x + 0.5f * hi.x, 0.5f * lo.y + 0.5f * hi.y, 0.5f * lo.z + 0.5f * hi.z));
+  const uint32_t lane = threadIdx.x & 63;
+  const f3 corner = mk((lane & 1) ? hi.x : lo.x, (lane & 2) ? hi.y + j : lo.y - j, (lane & 4) ? hi.z + j : lo.z - j);
+  const float lam = lane < 8 ? dot(dir(corner), b.a) : 3.0f;
+  b.c_lo = wave_min_all(lam) - 1e-5f;
+  b.c_hi = 1.00001f;
+  b.s_hi = __builtin_sqrtf(fmaxf(0.0f, 1.00002f - b.c_lo * b.c_lo)) * 1.00001f + 1e-6f;
+  ok = b.c_lo > 0.5f;  // a sane cap (NaN -> false)
+  return b;
+}
+
+// Bundle rules R3-R5 of camera-list records [base, base + 64) against b (lane j: record base + j).
+__device__ __forceinline__ bool bundle_keep(const float4* __restrict__ cr, uint32_t k, const Bundle& b) {
+  const float4 C0 = cr[5 * k], C1 = cr[5 * k + 1], C2 = cr[5 * k + 2], C3 = cr[5 * k + 3], C4 = cr[5 * k + 4];
+  const float na = dot(mk(C0.x, C0.y, C0.z), b.a), ua = dot(mk(C1.x, C1.y, C1.z), b.a);
+  const float va = dot(mk(C2.x, C2.y, C2.z), b.a), wa = dot(mk(C3.x, C3.y, C3.z), b.a);
+  const bool rej = (lin_lower(na, C4.x, b) > C0.w) | (lin_upper(ua, C4.y, b) < -C1.w) |
+                   (lin_lower(va, C4.z, b) > C2.w) | (lin_lower(wa, C4.w, b) > C3.w);
+  return !rej;
+}
+
+// Builds the wave's list (all 64 lanes active; the caller synchronises before reading it).
+__device__ __forceinline__ TileList build_tile_list(const TraceParams& P, uint32_t* slice, bool active, f3 centre) {
+  const hrt_push_constants& pc = P.pc;
+  TileList t{slice, 0u, false};
+  if (pc.num_meshes > 32 || !__any(active)) return t;
+  bool ok;
+  const Bundle b = tile_bundle(pc, active, centre, ok);
+  if (!ok) return t;
+  const uint32_t lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int m = 0; m < pc.num_meshes; ++m) {
+    const uint32_t k0 = P.cam_start[m], k1 = k0 + P.cam_count[m];
+    for (uint32_t base = k0; base < k1; base += 64) {
+      const uint32_t k = base + lane;
+      const bool keep = k < k1 && bundle_keep(P.cam_cull, k, b);
+      const unsigned long long mask = __ballot(keep);
+      const uint32_t cnt = (uint32_t)__popcll(mask);
+      if (t.n + cnt > kTileCap) return t;  // ok stays false: per-iteration cull
+      if (keep) slice[t.n + (uint32_t)__popcll(mask & below)] = k | ((uint32_t)m << 27);
+      t.n += cnt;
+    }
+  }
+  t.ok = true;
+  return t;
+}
+
+// Primary segments from the wave's list (ALL 64 lanes active).  Per lane: spheres, the meshes' AABB
+// quirk (raytracing.glsl:279) and its test count, then the listed triangles in buffer order.
+__device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParams& P, const TileList& tl, bool prim,
+                                               f3 o, f3 d, uint32_t& tests, Closest& c) {
+  const hrt_push_constants& pc = P.pc;
+  spheres_first(sc, pc, prim, o, d, c);
+  uint32_t pass_mask = 0;
+  if (prim) {
+    for (int m = 0; m < pc.num_meshes; ++m) {
+      if (aabb_pass(sc.meshes[m], o, d)) {
+        pass_mask |= 1u << m;
+        tests += sc.meshes[m].len;
+      }
+    }
+  }
+  float best_k = c.t * kOnePlus;
+  const kfloat* ct = to_const(P.cam_tris);
+  for (uint32_t i = 0; i < tl.n; ++i) {
+    const uint32_t e = __builtin_amdgcn_readfirstlane(tl.e[i]);
+    const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
+    const bool pass = (pass_mask >> m) & 1u;
+    if (!__any(pass)) continue;
+    const float4 N = ldk(ct, 4 * kk + 3);
+    const float dn = pass ? dot(d, mk(N.x, N.y, N.z)) : 0.0f;
+    if (__any(dn < 0.0f)) primary_exact(ct, kk, dn, d, m, c, best_k);
+  }
+}
+
 // Primary segments of the lanes with prim == true.  Called with ALL 64 lanes of the wave active.
 __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TraceParams& P, bool prim, f3 o, f3 d,
                                                  uint32_t& tests, Closest& c, Diag& dg) {
@@ -551,7 +665,7 @@ __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TracePar
   const Bundle b = make_bundle(prim, d);
   spheres_first(sc, pc, prim, o, d, c);
   float best_k = c.t * kOnePlus;
-  const float4* __restrict__ ct = P.cam_tris;
+  const kfloat* ct = to_const(P.cam_tris);
   const float4* __restrict__ cr = P.cam_cull;
   const uint32_t lane = threadIdx.x & 63;
   for (int m = 0; m < pc.num_meshes; ++m) {
@@ -577,10 +691,10 @@ __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TracePar
         dg.prim_survivors += (uint32_t)__popcll(mask);
       }
       while (mask) {
-        const uint32_t kk = base + (uint32_t)__builtin_ctzll(mask);
+        const uint32_t kk = __builtin_amdgcn_readfirstlane(base + (uint32_t)__builtin_ctzll(mask));
         mask &= mask - 1ull;
         if (pass) {
-          const float4 N = ct[4 * kk + 3];
+          const float4 N = ldk(ct, 4 * kk + 3);
           const float dn = dot(d, mk(N.x, N.y, N.z));
           if (__any(dn < 0.0f)) primary_exact(ct, kk, dn, d, (uint32_t)m, c, best_k);
         }
@@ -611,6 +725,7 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
   spheres_first(sc, pc, sec, o, d, c);
   float best_k = c.t * kOnePlus;
   const float4* __restrict__ T = reinterpret_cast<const float4*>(sc.tris);
+  const kfloat* Tk = to_const(T);
   const uint32_t lane = threadIdx.x & 63;
   for (int m = 0; m < pc.num_meshes; ++m) {
     const hrt_mesh& mesh = sc.meshes[m];
@@ -639,10 +754,11 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
         dg.sec_survivors += (uint32_t)__popcll(mask);
       }
       while (mask) {
-        const uint32_t kk = base + (uint32_t)__builtin_ctzll(mask);
+        // wave-uniform by construction: read through the constant address space -> s_load
+        const uint32_t kk = __builtin_amdgcn_readfirstlane(base + (uint32_t)__builtin_ctzll(mask));
         mask &= mask - 1ull;
-        if (pass) tri_two_stage(T[4 * kk], T[4 * kk + 1], T[4 * kk + 2], T[4 * kk + 3], kk, (uint32_t)m, o, d, c,
-                                best_k);
+        if (pass) tri_two_stage(ldk(Tk, 4 * kk), ldk(Tk, 4 * kk + 1), ldk(Tk, 4 * kk + 2), ldk(Tk, 4 * kk + 3), kk,
+                                (uint32_t)m, o, d, c, best_k);
       }
     }
   }
@@ -856,6 +972,12 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     centre = mk(rc.x, rc.y, rc.z);
   }
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
+  __shared__ uint32_t tile_lds[4 * kTileCap];
+  const TileList tl = build_tile_list(P, tile_lds + (threadIdx.x >> 6) * kTileCap, active, centre);
+  // The list is private to the wave and a wave's LDS accesses complete in order, so a wave-level
+  // barrier suffices (a __syncthreads() fence would also stop the compiler from scalarising the
+  // uniform scene loads that follow).
+  __builtin_amdgcn_wave_barrier();
   int sample = 0;
   Path p;
   p.bounce = pc.max_bounces + 1;
@@ -885,7 +1007,17 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
       dg.sec_lanes += run_sec ? nwait : 0u;
       t0 = __builtin_readcyclecounter();
     }
-    if (any_prim) world_hit_bundle(sc, P, prim, p.pos, p.dir, tests, c, dg);
+    if (any_prim) {
+      if (tl.ok) {
+        world_hit_tile(sc, P, tl, prim, p.pos, p.dir, tests, c);
+        if (P.diag) {
+          dg.prim_considered += tl.n;
+          dg.prim_survivors += tl.n;
+        }
+      } else {
+        world_hit_bundle(sc, P, prim, p.pos, p.dir, tests, c, dg);
+      }
+    }
     if (P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
       if constexpr (Bounce == kBounceBvh) {
