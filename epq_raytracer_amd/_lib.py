@@ -77,7 +77,7 @@ KERNEL_BUNDLE_BVH = 6
 KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull", 6: "bundle_bvh"}
 DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounce_iters", "bounce_considered",
               "bounce_survivors", "bounce_lanes", "bvh_visits", "bvh_prim_tests", "bvh_band_tests", "primary_cycles", "bounce_cycles",
-              "shade_cycles")
+              "shade_cycles", "bounce_stage2", "bounce_front")
 SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh_built", "bvh_band_entries")
 
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).

@@ -484,6 +484,7 @@ struct Diag {
   uint32_t sec_iters = 0, sec_considered = 0, sec_survivors = 0, sec_lanes = 0;
   uint32_t bvh_visits = 0, bvh_prims = 0, bvh_band = 0;  // per lane (BUNDLE_BVH)
   uint64_t cyc_prim = 0, cyc_sec = 0, cyc_shade = 0;  // shader clocks per wave and phase
+  uint32_t sec_stage2 = 0, sec_front = 0;                // bounce survivors reaching stage 2 / with a front-facing lane
 };
 
 __device__ __forceinline__ float wave_min_all(float v) {  // all 64 lanes active
@@ -757,6 +758,13 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
         // wave-uniform by construction: read through the constant address space -> s_load
         const uint32_t kk = __builtin_amdgcn_readfirstlane(base + (uint32_t)__builtin_ctzll(mask));
         mask &= mask - 1ull;
+        if (P.diag && pass) {  // how far the two-stage test gets for this survivor
+          const float4 A = ldk(Tk, 4 * kk), N = ldk(Tk, 4 * kk + 3);
+          const f3 ao = o - mk(A.x, A.y, A.z);
+          const bool s2 = dot(ao, mk(N.x, N.y, N.z)) > 0.0f;
+          dg.sec_stage2 += __any(s2) ? 1u : 0u;
+          dg.sec_front += __any(s2 && dot(d, mk(N.x, N.y, N.z)) < 0.0f) ? 1u : 0u;
+        }
         if (pass) tri_two_stage(ldk(Tk, 4 * kk), ldk(Tk, 4 * kk + 1), ldk(Tk, 4 * kk + 2), ldk(Tk, 4 * kk + 3), kk,
                                 (uint32_t)m, o, d, c, best_k);
       }
@@ -1054,6 +1062,8 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[10], (unsigned long long)dg.cyc_prim);
     atomicAdd(&P.diag[11], (unsigned long long)dg.cyc_sec);
     atomicAdd(&P.diag[12], (unsigned long long)dg.cyc_shade);
+    atomicAdd(&P.diag[13], (unsigned long long)dg.sec_stage2);
+    atomicAdd(&P.diag[14], (unsigned long long)dg.sec_front);
     atomicAdd(&P.diag[0], (unsigned long long)dg.prim_iters);
     atomicAdd(&P.diag[1], (unsigned long long)dg.prim_considered);
     atomicAdd(&P.diag[2], (unsigned long long)dg.prim_survivors);

@@ -190,7 +190,9 @@ typedef enum hrt_diag {
   HRT_DIAG_PRIMARY_CYCLES = 10,    /* shader clocks per wave in the primary cull + tests, summed */
   HRT_DIAG_BOUNCE_CYCLES = 11,     /* ... in the bounce-batch path */
   HRT_DIAG_SHADE_CYCLES = 12,      /* ... in shading (scatter, RNG, colour) */
-  HRT_NUM_DIAG = 13
+  HRT_DIAG_BOUNCE_STAGE2 = 13,     /* BUNDLE_CULL: bounce survivors with some lane's num_t > 0 */
+  HRT_DIAG_BOUNCE_FRONT = 14,      /* ... and some such lane front-facing (dn < 0) */
+  HRT_NUM_DIAG = 15
 } hrt_diag;
 
 /* What hrt_set_scene built for BUNDLE_BVH (hrt_get_scene_info). */

@@ -78,6 +78,8 @@ def main():
                 for ph in ("primary", "bounce", "shade"):
                     d[ph + "_cycle_share"] = d[ph + "_cycles"] / max(cyc, 1)
                 d["bounce_cycles_per_iter"] = d["bounce_cycles"] / max(d["bounce_iters"], 1)
+                d["bounce_stage2_frac"] = d["bounce_stage2"] / max(d["bounce_survivors"], 1)
+                d["bounce_front_frac"] = d["bounce_front"] / max(d["bounce_survivors"], 1)
                 d["primary_cycles_per_iter"] = d["primary_cycles"] / max(d["primary_iters"], 1)
                 print(json.dumps(d), flush=True)
                 ctx.set_option(_lib.OPT_COUNTERS, 1)

@@ -93,8 +93,8 @@ def main():
             with open(os.path.join(a.out, "p1.log")) as fh:
                 for line in fh:
                     if line.startswith("{"):
-                        ref_tests = json.loads(line)["tri_tests"]
-        except (OSError, ValueError, KeyError):
+                        ref_tests = json.loads(line).get("tri_tests", ref_tests)
+        except (OSError, ValueError):
             pass
         with open(a.traffic_json, "w") as f:
             json.dump({"workload": wl, "kernel": k, "hbm_bytes_per_trace_launch": d.get("hbm_bytes"),
