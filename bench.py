@@ -28,8 +28,6 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
 FLOP_PER_TEST = 38         # algorithmic fp32 FLOP per ray-triangle test (raytracing.glsl:213-241)
 BYTES_PER_PIXEL_FRAME = 32  # 16 B ray centre + 4 B trace store + 12 B combiner (r, r, w)
-KERNEL_SYMBOLS = {0: "hrt::trace_bundle_cull", 1: "hrt::trace_literal", 2: "hrt::trace_brute",
-                  3: "hrt::trace_brute_lds", 4: "hrt::trace_bundle", 5: "hrt::trace_bundle_cull"}
 
 
 def parse():
@@ -124,6 +122,7 @@ def main():
     st = ctx.stats()
     segs, tests = st.segments, st.tri_tests
     kern_ms = st.total_trace_ms / max(st.traces, 1)
+    kernel_sym = _lib.kernel_symbol(st.last_kernel, st.last_block)  # what HRT_KERNEL_AUTO resolved to
     if dist_on:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -152,7 +151,8 @@ def main():
                 pmc = json.load(f)
             wl = pmc.get("workload", {})
             if (wl.get("scene"), wl.get("width"), wl.get("height"), wl.get("spp"), wl.get("bounces"),
-                    wl.get("variant")) == (args.scene, W, H, args.spp, args.bounces, args.variant):
+                    wl.get("variant"), pmc.get("kernel")) == (args.scene, W, H, args.spp, args.bounces, args.variant,
+                                                              kernel_sym):
                 per_test = pmc.get("executed_flops_per_reference_test")
                 if world == 1:
                     traffic = pmc.get("hbm_bytes_per_trace_launch")
@@ -196,7 +196,7 @@ def main():
                          "achieved_basis": "executed (rocprofv3 PMC FLOP count per launch / live launch time)"
                                            if executed_flops else "reference-equivalent (38 FLOP x reference tests)",
                          "algorithmic_tflops": round(algorithmic_tf, 3),
-                         "kernel": KERNEL_SYMBOLS[args.variant],
+                         "kernel": kernel_sym,
                          "kernel_ms": round(kern_ms, 3), "flop_per_test": FLOP_PER_TEST,
                          "tests_per_launch": int(tests_per_launch), "pmc_source": pmc_note},
             "hbm_roofline": {"achieved": round(algo_bytes / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,

@@ -61,7 +61,8 @@ class Layout(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("segments", c_uint64), ("tri_tests", c_uint64), ("traces", c_uint64), ("accumulates", c_uint64),
-                ("last_trace_ms", c_float), ("total_trace_ms", c_float), ("wave_steps", c_uint64)]
+                ("last_trace_ms", c_float), ("total_trace_ms", c_float), ("wave_steps", c_uint64),
+                ("last_kernel", c_uint32), ("last_block", c_uint32)]
 
 
 HRT_OK = 0
@@ -73,11 +74,22 @@ FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
 # hrt_kernel (include/hip_raytrace.h)
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
-KERNEL_BUNDLE_BVH = 6
-KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull", 6: "bundle_bvh"}
+KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS = 6, 7
+# kernel symbol (as rocprofv3 names it) of a resolved hrt_kernel + workgroup size
+def kernel_symbol(kernel: int, block: int) -> str:
+    base = {1: "trace_literal", 2: "trace_brute", 3: "trace_brute_lds", 4: "trace_bundle", 5: "trace_bundle_cull",
+            6: "trace_bundle_bvh"}
+    if kernel == 7:
+        return f"void hrt::trace_bundle_cull_lds<{block}>(hrt::TraceParams)"
+    return f"hrt::{base.get(kernel, '?')}(hrt::TraceParams)"
+
+
+KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull", 6: "bundle_bvh",
+                7: "bundle_cull_lds"}
 DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounce_iters", "bounce_considered",
               "bounce_survivors", "bounce_lanes", "bvh_visits", "bvh_prim_tests", "bvh_band_tests", "primary_cycles", "bounce_cycles",
-              "shade_cycles", "bounce_stage2", "bounce_front")
+              "shade_cycles", "bounce_stage2", "bounce_front", "bvh_trips",
+              "bvh_leaf_trips")
 SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh_built", "bvh_band_entries")
 
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).

@@ -72,6 +72,7 @@ struct hrt_context {
   bool counters_on = true;
   bool diag_on = false;
   uint32_t sec_batch = 48;
+  int last_kernel = 0, last_block = 0;  // what the last hrt_trace launched (hrt_stats)
 
   std::vector<EventPair> event_pool;     // reusable
   std::vector<EventPair> pending;        // recorded, not yet harvested
@@ -370,7 +371,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
     HRT_HIP(ctx, hipEventCreate(&ev.stop));
   }
   HRT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
-  hipError_t e = hrt::launch_trace(p, variant, ctx->stream);
+  hipError_t e = hrt::launch_trace(p, variant, ctx->stream, &ctx->last_kernel, &ctx->last_block);
   if (e != hipSuccess) {
     ctx->event_pool.push_back(ev);
     return hip_fail(ctx, e, "trace kernel launch");
@@ -459,6 +460,8 @@ extern "C" hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out) {
   out->traces = ctx->traces;
   out->accumulates = ctx->accumulates;
   out->wave_steps = c[2];
+  out->last_kernel = (uint32_t)ctx->last_kernel;
+  out->last_block = (uint32_t)ctx->last_block;
   out->last_trace_ms = ctx->last_ms;
   out->total_trace_ms = ctx->total_ms;
   return HRT_OK;
@@ -496,8 +499,8 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   switch (key) {
     case HRT_OPT_KERNEL_VARIANT:
-      if (value < HRT_KERNEL_AUTO || value > HRT_KERNEL_BUNDLE_BVH)
-        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be an hrt_kernel value (0..6)");
+      if (value < HRT_KERNEL_AUTO || value > HRT_KERNEL_BUNDLE_CULL_LDS)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be an hrt_kernel value (0..7)");
       ctx->variant = (int)value;
       return HRT_OK;
     case HRT_OPT_COUNTERS:

@@ -28,6 +28,7 @@ struct TraceParams {
   float4* cam_tris;              // 4 float4 per record: (ao, num_t) (e1, index bits) (e2, -) (n, -)
   float4* cam_cull;              // 5 float4 per record: bundle-cull linear forms + margins
   uint32_t sec_batch;            // bounce segments run once this many lanes of a wave wait (1..64)
+  uint32_t lds_tile_cap;         // BUNDLE_CULL_LDS: primary-list entries per wave (set by launch_trace)
   // BUNDLE_BVH: bounce-segment hierarchy built by hrt_set_scene (hrt_bvh.h records); nullptr = none.
   const float4* bvh_nodes;       // 4 float4 per node, preorder with escape indices
   const float4* bvh_prims;       // 4 float4 per leaf triangle
@@ -37,7 +38,8 @@ struct TraceParams {
   uint32_t bvh_n_nodes, bvh_n_irregular;
 };
 
-hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream);
+// Launches the trace kernel(s); *ran / *block receive the resolved hrt_kernel and workgroup size.
+hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, int* ran, int* block);
 int resolve_variant(const TraceParams& p, int variant);  // the kernel an HRT_KERNEL_* request runs
 hipError_t launch_clear(uint32_t* img8, float4* img32, size_t npix, hipStream_t stream);
 hipError_t launch_accumulate(uint32_t* cur8, const uint32_t* new8, float4* cur32, const float4* new32, size_t npix,

@@ -19,6 +19,8 @@
 //   BUNDLE_CULL  BUNDLE + a lane-parallel origin-box / direction-cone pre-cull for bounce segments.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "hip_raytrace.h"
 #include "hrt_bvh.h"
 #include "hrt_kernels.h"
@@ -484,12 +486,18 @@ struct Diag {
   uint32_t sec_iters = 0, sec_considered = 0, sec_survivors = 0, sec_lanes = 0;
   uint32_t bvh_visits = 0, bvh_prims = 0, bvh_band = 0;  // per lane (BUNDLE_BVH)
   uint64_t cyc_prim = 0, cyc_sec = 0, cyc_shade = 0;  // shader clocks per wave and phase
-  uint32_t sec_stage2 = 0, sec_front = 0;                // bounce survivors reaching stage 2 / with a front-facing lane
+  uint32_t sec_stage2 = 0, sec_front = 0;
+  uint32_t bvh_trips = 0, bvh_leaf_trips = 0;  // BUNDLE_BVH: wave-level traversal trips                // bounce survivors reaching stage 2 / with a front-facing lane
 };
 
 __device__ __forceinline__ float wave_min_all(float v) {  // all 64 lanes active
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {  // all 64 lanes active
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
   return v;
 }
 __device__ __forceinline__ float wave_max_all(float v) {
@@ -606,7 +614,8 @@ __device__ __forceinline__ bool bundle_keep(const float4* __restrict__ cr, uint3
 }
 
 // Builds the wave's list (all 64 lanes active; the caller synchronises before reading it).
-__device__ __forceinline__ TileList build_tile_list(const TraceParams& P, uint32_t* slice, bool active, f3 centre) {
+__device__ __forceinline__ TileList build_tile_list(const TraceParams& P, uint32_t* slice, uint32_t cap, bool active,
+                                                   f3 centre) {
   const hrt_push_constants& pc = P.pc;
   TileList t{slice, 0u, false};
   if (pc.num_meshes > 32 || !__any(active)) return t;
@@ -622,7 +631,7 @@ __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, uint32
       const bool keep = k < k1 && bundle_keep(P.cam_cull, k, b);
       const unsigned long long mask = __ballot(keep);
       const uint32_t cnt = (uint32_t)__popcll(mask);
-      if (t.n + cnt > kTileCap) return t;  // ok stays false: per-iteration cull
+      if (t.n + cnt > cap) return t;  // ok stays false: per-iteration cull
       if (keep) slice[t.n + (uint32_t)__popcll(mask & below)] = k | ((uint32_t)m << 27);
       t.n += cnt;
     }
@@ -704,6 +713,34 @@ __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TracePar
   }
 }
 
+// Triangle sources of the bounce cull: lane(k) -> (a, n) of triangle k for the lane-parallel cull,
+// uniform(k) -> (a, e1, e2, n) of a wave-uniform survivor.
+struct CullGlobal {  // std430 buffer; survivors through the constant address space (s_load)
+  const float4* __restrict__ T;
+  const kfloat* Tk;
+  __device__ __forceinline__ void lane(uint32_t k, float4& A, float4& N) const {
+    A = T[4 * k];
+    N = T[4 * k + 3];
+  }
+  __device__ __forceinline__ void uniform(uint32_t k, float4& A, float4& B, float4& C, float4& N) const {
+    A = ldk(Tk, 4 * k);
+    B = ldk(Tk, 4 * k + 1);
+    C = ldk(Tk, 4 * k + 2);
+    N = ldk(Tk, 4 * k + 3);
+  }
+};
+struct CullLds {  // LDS image, 3 float4 per triangle: (a, n.x) (n.yz, e1.xy) (e1.z, e2)
+  const float4* t;
+  __device__ __forceinline__ void lane(uint32_t k, float4& A, float4& N) const {
+    const float4 p = t[3 * k], q = t[3 * k + 1];
+    A = make_float4(p.x, p.y, p.z, 0.0f);
+    N = make_float4(p.w, q.x, q.y, 0.0f);
+  }
+  __device__ __forceinline__ void uniform(uint32_t k, float4& A, float4& B, float4& C, float4& N) const {
+    LdsTris{t}(k, A, B, C, N);
+  }
+};
+
 // Bounce segments with a lane-parallel pre-cull (BUNDLE_CULL).  For the bounce lanes (origins o_l,
 // directions d_l) and triangle (a, n):
 //   S1  num_t = (o - a).n is linear in o: if max over the lanes' origin box B of (o - a).n
@@ -712,8 +749,9 @@ __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TracePar
 //       lane has dn >= 0: rejected.
 // Lane j bounds triangle base+j; survivors (buffer order) get the exact per-lane two-stage test.
 // Called with ALL 64 lanes active.
-__device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const TraceParams& P, bool sec, f3 o, f3 d,
-                                                      uint32_t& tests, Closest& c, Diag& dg) {
+template <class Src>
+__device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const TraceParams& P, const Src& src, bool sec,
+                                                      f3 o, f3 d, uint32_t& tests, Closest& c, Diag& dg) {
   const hrt_push_constants& pc = P.pc;
   const float inf = __builtin_inff();
   const f3 lo = mk(wave_min_all(sec ? o.x : inf), wave_min_all(sec ? o.y : inf), wave_min_all(sec ? o.z : inf));
@@ -725,8 +763,6 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
   const f3 hw = mk((hi.x - ctr.x) * 1.0001f, (hi.y - ctr.y) * 1.0001f, (hi.z - ctr.z) * 1.0001f);
   spheres_first(sc, pc, sec, o, d, c);
   float best_k = c.t * kOnePlus;
-  const float4* __restrict__ T = reinterpret_cast<const float4*>(sc.tris);
-  const kfloat* Tk = to_const(T);
   const uint32_t lane = threadIdx.x & 63;
   for (int m = 0; m < pc.num_meshes; ++m) {
     const hrt_mesh& mesh = sc.meshes[m];
@@ -738,7 +774,8 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
       const uint32_t k = base + lane;
       bool keep = false;
       if (k < k1) {
-        const float4 A = T[4 * k], N = T[4 * k + 3];
+        float4 A, N;
+        src.lane(k, A, N);
         const f3 n = mk(N.x, N.y, N.z);
         const f3 ca = ctr - mk(A.x, A.y, A.z);
         const float an = fabsf(n.x), bn = fabsf(n.y), cn = fabsf(n.z);
@@ -755,18 +792,18 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
         dg.sec_survivors += (uint32_t)__popcll(mask);
       }
       while (mask) {
-        // wave-uniform by construction: read through the constant address space -> s_load
+        // wave-uniform by construction (global source: constant address space -> s_load)
         const uint32_t kk = __builtin_amdgcn_readfirstlane(base + (uint32_t)__builtin_ctzll(mask));
         mask &= mask - 1ull;
+        float4 A, B, C, N;
+        src.uniform(kk, A, B, C, N);
         if (P.diag && pass) {  // how far the two-stage test gets for this survivor
-          const float4 A = ldk(Tk, 4 * kk), N = ldk(Tk, 4 * kk + 3);
           const f3 ao = o - mk(A.x, A.y, A.z);
           const bool s2 = dot(ao, mk(N.x, N.y, N.z)) > 0.0f;
           dg.sec_stage2 += __any(s2) ? 1u : 0u;
           dg.sec_front += __any(s2 && dot(d, mk(N.x, N.y, N.z)) < 0.0f) ? 1u : 0u;
         }
-        if (pass) tri_two_stage(ldk(Tk, 4 * kk), ldk(Tk, 4 * kk + 1), ldk(Tk, 4 * kk + 2), ldk(Tk, 4 * kk + 3), kk,
-                                (uint32_t)m, o, d, c, best_k);
+        if (pass) tri_two_stage(A, B, C, N, kk, (uint32_t)m, o, d, c, best_k);
       }
     }
   }
@@ -935,13 +972,16 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
       }
     }
   }
+  uint32_t trips = 0, leaf_trips = 0;  // wave-level loop iterations (diagnostics)
   while (node < end) {
+    if (P.diag) ++trips;
     const float4 N0 = nodes[4 * node], N1 = nodes[4 * node + 1], N2 = nodes[4 * node + 2], N3 = nodes[4 * node + 3];
     const uint32_t info = __builtin_bit_cast(uint32_t, N3.z);
     const uint32_t esc = __builtin_bit_cast(uint32_t, N3.w);
     const bool visit = bvh_node_visit(N0, N1, N2, N3, o, d, inv, c.t);
     const uint32_t count = info >> 27;
     ++visits;
+    if (P.diag && __any(visit && count)) ++leaf_trips;
     if (visit && count) {
       const uint32_t first = info & 0x07FFFFFFu;
       for (uint32_t k = first; k < first + count; ++k) bvh_prim_test(P.bvh_prims, k, mask, o, d, c, bkey, best_k);
@@ -953,6 +993,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
     dg.bvh_visits += visits;
     dg.bvh_prims += prim_tests;
     dg.bvh_band += band_tests;
+    // trips run by the whole wave: the maximum over its lanes (the loop is divergent)
+    dg.bvh_trips += wave_max_u(trips);
+    dg.bvh_leaf_trips += wave_max_u(leaf_trips);
   }
 }
 
@@ -963,8 +1006,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
 enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2 };
 
-template <int Bounce>
-__device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr) {
+template <int Bounce, class CullSrc>
+__device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, uint32_t* tile_slice,
+                                                  uint32_t tile_cap, const CullSrc& csrc) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
   const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
@@ -980,8 +1024,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     centre = mk(rc.x, rc.y, rc.z);
   }
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
-  __shared__ uint32_t tile_lds[4 * kTileCap];
-  const TileList tl = build_tile_list(P, tile_lds + (threadIdx.x >> 6) * kTileCap, active, centre);
+  const TileList tl = build_tile_list(P, tile_slice, tile_cap, active, centre);
   // The list is private to the wave and a wave's LDS accesses complete in order, so a wave-level
   // barrier suffices (a __syncthreads() fence would also stop the compiler from scalarising the
   // uniform scene loads that follow).
@@ -1031,7 +1074,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
       if constexpr (Bounce == kBounceBvh) {
         world_hit_bounce_bvh(sc, P, sec, p.pos, p.dir, tests, c, dg);
       } else if constexpr (Bounce == kBounceCull) {
-        world_hit_bounce_cull(sc, P, sec, p.pos, p.dir, tests, c, dg);
+        world_hit_bounce_cull(sc, P, csrc, sec, p.pos, p.dir, tests, c, dg);
       } else {
         if (sec) c = world_hit_brute(sc, src, pc, p.pos, p.dir, tests);
       }
@@ -1064,6 +1107,8 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[12], (unsigned long long)dg.cyc_shade);
     atomicAdd(&P.diag[13], (unsigned long long)dg.sec_stage2);
     atomicAdd(&P.diag[14], (unsigned long long)dg.sec_front);
+    atomicAdd(&P.diag[15], (unsigned long long)dg.bvh_trips);
+    atomicAdd(&P.diag[16], (unsigned long long)dg.bvh_leaf_trips);
     atomicAdd(&P.diag[0], (unsigned long long)dg.prim_iters);
     atomicAdd(&P.diag[1], (unsigned long long)dg.prim_considered);
     atomicAdd(&P.diag[2], (unsigned long long)dg.prim_survivors);
@@ -1080,9 +1125,12 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
 }
 
 __global__ __launch_bounds__(256) void trace_bundle(TraceParams P) {
+  __shared__ uint32_t tile_lds[4 * kTileCap];
   uint32_t x, lr;
   lane_pixel(P, x, lr);
-  trace_fused_split<kBounceBrute>(P, x, lr);
+  const float4* T = reinterpret_cast<const float4*>(P.tris);
+  trace_fused_split<kBounceBrute>(P, x, lr, tile_lds + (threadIdx.x >> 6) * kTileCap, kTileCap,
+                                  CullGlobal{T, to_const(T)});
 }
 
 #ifndef HRT_CULL_WAVES
@@ -1090,15 +1138,44 @@ __global__ __launch_bounds__(256) void trace_bundle(TraceParams P) {
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HRT_CULL_WAVES))) void trace_bundle_cull(
     TraceParams P) {
+  __shared__ uint32_t tile_lds[4 * kTileCap];
   uint32_t x, lr;
   lane_pixel(P, x, lr);
-  trace_fused_split<kBounceCull>(P, x, lr);
+  const float4* T = reinterpret_cast<const float4*>(P.tris);
+  trace_fused_split<kBounceCull>(P, x, lr, tile_lds + (threadIdx.x >> 6) * kTileCap, kTileCap,
+                                 CullGlobal{T, to_const(T)});
 }
 
 __global__ __launch_bounds__(256) void trace_bundle_bvh(TraceParams P) {
+  __shared__ uint32_t tile_lds[4 * kTileCap];
   uint32_t x, lr;
   lane_pixel(P, x, lr);
-  trace_fused_split<kBounceBvh>(P, x, lr);
+  const float4* T = reinterpret_cast<const float4*>(P.tris);
+  trace_fused_split<kBounceBvh>(P, x, lr, tile_lds + (threadIdx.x >> 6) * kTileCap, kTileCap,
+                                CullGlobal{T, to_const(T)});
+}
+
+// BUNDLE_CULL with the triangles resident in LDS (bounce survivors are read at LDS rather than L2
+// latency).  Dynamic LDS: [n_tris x 48 B triangles][waves x tile_cap x 4 B primary lists].
+// Workgroups of BLOCK threads cover (BLOCK/64 waves) 8x8 tiles: 512 -> 32x16 pixels, 1024 -> 32x32.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
+  const uint32_t n = P.n_tris;
+  for (uint32_t k = threadIdx.x; k < 3 * n; k += BLOCK) {
+    const uint32_t i = k / 3, part = k - 3 * i;
+    const hrt_triangle& t = P.tris[i];
+    float4 v;
+    if (part == 0) v = make_float4(t.a[0], t.a[1], t.a[2], t.normal[0]);
+    else if (part == 1) v = make_float4(t.normal[1], t.normal[2], t.edge_one[0], t.edge_one[1]);
+    else v = make_float4(t.edge_one[2], t.edge_two[0], t.edge_two[1], t.edge_two[2]);
+    lds_tris[k] = v;
+  }
+  __syncthreads();
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t x = blockIdx.x * 32 + (wave & 3) * 8 + (lane & 7);
+  const uint32_t lr = blockIdx.y * (BLOCK / 32) + (wave >> 2) * 8 + (lane >> 3);
+  uint32_t* lists = reinterpret_cast<uint32_t*>(lds_tris + 3 * n);
+  trace_fused_split<kBounceCull>(P, x, lr, lists + wave * P.lds_tile_cap, P.lds_tile_cap, CullLds{lds_tris});
 }
 
 // Per-frame prep for the bundle variants: one workgroup per mesh, order-preserving compaction of the
@@ -1227,26 +1304,53 @@ constexpr size_t kMaxLdsScene = 160 * 1024;
 constexpr uint32_t kAutoCullTris = 256;   // BUNDLE_CULL from this many mesh triangles, BUNDLE below
 constexpr uint32_t kAutoBvhTris = 4096;   // BUNDLE_BVH from this many (profiles/r01d_bvh_scaling.log)
 
+// BUNDLE_CULL_LDS workgroup size for a scene of n triangles (0 = does not fit) and the per-wave
+// primary-list capacity left over: two 512-thread workgroups per CU when twice the footprint fits the
+// 160 KiB, else one of 1024.
+uint32_t lds_block(uint32_t n, uint32_t* cap) {
+  constexpr size_t kMinCap = 16;
+  const size_t tri = (size_t)n * 48;
+  uint32_t block = 0, c = 0;
+  if (tri + 8 * kMinCap * 4 <= kMaxLdsScene / 2) {
+    block = 512;
+    c = (uint32_t)std::min<size_t>(kTileCap, (kMaxLdsScene / 2 - tri) / (8 * 4));
+  } else if (tri + 16 * kMinCap * 4 <= kMaxLdsScene) {
+    block = 1024;
+    c = (uint32_t)std::min<size_t>(kTileCap, (kMaxLdsScene - tri) / (16 * 4));
+  }
+  if (cap) *cap = c;
+  return block;
+}
+
 int resolve_variant(const TraceParams& p, int variant) {
   if (variant == HRT_KERNEL_AUTO) {
+    // profiles/r01g_*: island 21.4 (LDS) vs 23.7 ms, cave 112 vs 120 ms; BVH from ~4K triangles
     variant = p.cam_list_capacity >= kAutoBvhTris && p.bvh_nodes ? HRT_KERNEL_BUNDLE_BVH
-              : p.cam_list_capacity >= kAutoCullTris             ? HRT_KERNEL_BUNDLE_CULL
-                                                                 : HRT_KERNEL_BUNDLE;
+              : p.cam_list_capacity < kAutoCullTris              ? HRT_KERNEL_BUNDLE
+              : lds_block(p.n_tris, nullptr) != 0                ? HRT_KERNEL_BUNDLE_CULL_LDS
+                                                                 : HRT_KERNEL_BUNDLE_CULL;
   }
   if (variant == HRT_KERNEL_BRUTE_LDS && (size_t)p.n_tris * 48 > kMaxLdsScene) variant = HRT_KERNEL_BRUTE;
   if (variant == HRT_KERNEL_BUNDLE_BVH && (!p.bvh_nodes || p.pc.num_meshes > 64)) variant = HRT_KERNEL_BUNDLE_CULL;
+  if (variant == HRT_KERNEL_BUNDLE_CULL_LDS && lds_block(p.n_tris, nullptr) == 0) variant = HRT_KERNEL_BUNDLE_CULL;
   if (p.pc.max_bounces < 0) variant = HRT_KERNEL_LITERAL;  // the fused loops assume >= 1 segment per path
   return variant;
 }
 
-hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream) {
+hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, int* ran, int* block_out) {
   static bool lds_attr = false;
   if (!lds_attr) {
     lds_attr = true;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_brute_lds),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_bundle_cull_lds<512>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kMaxLdsScene / 2));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
   }
   variant = resolve_variant(p, variant);
+  *ran = variant;
+  *block_out = variant == HRT_KERNEL_BRUTE_LDS ? 1024 : 256;
   const dim3 grid((p.pc.width + 15) / 16, (p.local_rows + 15) / 16, 1);
   switch (variant) {
     case HRT_KERNEL_LITERAL:
@@ -1255,6 +1359,21 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream) {
     case HRT_KERNEL_BRUTE_LDS: {
       const dim3 g32((p.pc.width + 31) / 32, (p.local_rows + 31) / 32, 1);
       trace_brute_lds<<<g32, 1024, (size_t)p.n_tris * 48, stream>>>(p);
+      break;
+    }
+    case HRT_KERNEL_BUNDLE_CULL_LDS: {
+      if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      TraceParams q = p;
+      const uint32_t block = lds_block(p.n_tris, &q.lds_tile_cap);
+      *block_out = (int)block;
+      const size_t lds = (size_t)p.n_tris * 48 + (size_t)(block / 64) * q.lds_tile_cap * 4;
+      if (block == 512) {
+        const dim3 g((p.pc.width + 31) / 32, (p.local_rows + 15) / 16, 1);
+        trace_bundle_cull_lds<512><<<g, 512, lds, stream>>>(q);
+      } else {
+        const dim3 g((p.pc.width + 31) / 32, (p.local_rows + 31) / 32, 1);
+        trace_bundle_cull_lds<1024><<<g, 1024, lds, stream>>>(q);
+      }
       break;
     }
     case HRT_KERNEL_BUNDLE:

@@ -143,6 +143,8 @@ typedef struct hrt_stats {
   float total_trace_ms;   /* device time of all trace dispatches since reset */
   uint64_t wave_steps;    /* sum over waves of the wave's longest per-lane segment count: lane
                              efficiency = segments / (64 * wave_steps) */
+  uint32_t last_kernel;   /* hrt_kernel the last trace ran (HRT_KERNEL_AUTO resolved) */
+  uint32_t last_block;    /* its workgroup size (threads) */
 } hrt_stats;
 
 typedef struct hrt_context hrt_context;
@@ -150,15 +152,18 @@ typedef struct hrt_context hrt_context;
 /* Trace kernel variants (HRT_OPT_KERNEL_VARIANT).  All produce byte-identical frames and counters;
  * they differ only in how much of the reference's brute-force work they prove unnecessary. */
 typedef enum hrt_kernel {
-  HRT_KERNEL_AUTO = 0,        /* BUNDLE below 256 mesh triangles, BUNDLE_CULL below 4096, BUNDLE_BVH above */
+  HRT_KERNEL_AUTO = 0,        /* BUNDLE below 256 mesh triangles; then BUNDLE_CULL_LDS while the triangle
+                                 buffer fits LDS (else BUNDLE_CULL) below 4096; BUNDLE_BVH above */
   HRT_KERNEL_LITERAL = 1,     /* raytracing.glsl's loop shape, the full test on every triangle */
   HRT_KERNEL_BRUTE = 2,       /* fused sample/bounce loop, two-stage exact pre-test, triangles via SGPRs */
   HRT_KERNEL_BRUTE_LDS = 3,   /* BRUTE with the scene resident in LDS (falls back to BRUTE above 160 KiB) */
   HRT_KERNEL_BUNDLE = 4,      /* primary rays: lane-parallel bundle cull; bounces: deferred, BRUTE test */
   HRT_KERNEL_BUNDLE_CULL = 5, /* BUNDLE + lane-parallel origin-box / direction-cone cull of bounce rays */
-  HRT_KERNEL_BUNDLE_BVH = 6   /* BUNDLE + per-lane BVH traversal of bounce rays (hierarchy built by
+  HRT_KERNEL_BUNDLE_BVH = 6,  /* BUNDLE + per-lane BVH traversal of bounce rays (hierarchy built by
                                  hrt_set_scene; falls back to BUNDLE_CULL above 64 meshes or 2^18
                                  mesh triangles) */
+  HRT_KERNEL_BUNDLE_CULL_LDS = 7 /* BUNDLE_CULL with the triangle buffer resident in LDS (512/1024-thread
+                                    workgroups; falls back to BUNDLE_CULL above ~3,300 triangles) */
 } hrt_kernel;
 
 /* Option keys for hrt_set_option. */
@@ -192,7 +197,9 @@ typedef enum hrt_diag {
   HRT_DIAG_SHADE_CYCLES = 12,      /* ... in shading (scatter, RNG, colour) */
   HRT_DIAG_BOUNCE_STAGE2 = 13,     /* BUNDLE_CULL: bounce survivors with some lane's num_t > 0 */
   HRT_DIAG_BOUNCE_FRONT = 14,      /* ... and some such lane front-facing (dn < 0) */
-  HRT_NUM_DIAG = 15
+  HRT_DIAG_BVH_TRIPS = 15,         /* BUNDLE_BVH: traversal loop iterations per bounce batch (wave), summed */
+  HRT_DIAG_BVH_LEAF_TRIPS = 16,    /* ... of which some lane tested a leaf */
+  HRT_NUM_DIAG = 17
 } hrt_diag;
 
 /* What hrt_set_scene built for BUNDLE_BVH (hrt_get_scene_info). */

@@ -14,7 +14,7 @@ from helpers import E, SceneCase, _lib, mismatch_report
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [0, 1]  # auto (tuned), literal
-ALL_VARIANTS = list(range(7))  # every hrt_kernel value (hrt_set_option HRT_OPT_KERNEL_VARIANT)
+ALL_VARIANTS = list(range(8))  # every hrt_kernel value (hrt_set_option HRT_OPT_KERNEL_VARIANT)
 
 CONFIGS = [
     # (scene, size, spp, bounces, rng_offset)

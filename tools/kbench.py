@@ -44,7 +44,7 @@ def main():
         ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
         ctx.trace(pc)
         ref = ctx.read(_lib.IMG_TRACE)
-    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v in (0, 4, 5, 6) else [a.sec_batch[0]])]
+    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v in (0, 4, 5, 6, 7) else [a.sec_batch[0]])]
     res = {vs: [] for vs in combos}
     stats = {}
     same = {}
@@ -61,7 +61,7 @@ def main():
                 same[(v, sb)] = None if ref is None else bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
     if a.diag:
         for v in a.variants:
-            if v in (0, 4, 5, 6):
+            if v in (0, 4, 5, 6, 7):
                 ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
                 ctx.set_option(_lib.OPT_COUNTERS, 2)
                 ctx.reset_stats()
@@ -80,7 +80,10 @@ def main():
                 d["bounce_cycles_per_iter"] = d["bounce_cycles"] / max(d["bounce_iters"], 1)
                 d["bounce_stage2_frac"] = d["bounce_stage2"] / max(d["bounce_survivors"], 1)
                 d["bounce_front_frac"] = d["bounce_front"] / max(d["bounce_survivors"], 1)
+                d["bvh_trips_per_iter"] = d["bvh_trips"] / max(d["bounce_iters"], 1)
+                d["bvh_leaf_trips_per_iter"] = d["bvh_leaf_trips"] / max(d["bounce_iters"], 1)
                 d["primary_cycles_per_iter"] = d["primary_cycles"] / max(d["primary_iters"], 1)
+                d["primary_list_len"] = d["primary_considered"] / max(d["primary_iters"], 1)
                 print(json.dumps(d), flush=True)
                 ctx.set_option(_lib.OPT_COUNTERS, 1)
     out = []
