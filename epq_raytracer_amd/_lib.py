@@ -74,18 +74,20 @@ FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
 # hrt_kernel (include/hip_raytrace.h)
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
-KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS = 6, 7
+KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS, KERNEL_BUNDLE_BVH_LDS = 6, 7, 8
 # kernel symbol (as rocprofv3 names it) of a resolved hrt_kernel + workgroup size
 def kernel_symbol(kernel: int, block: int) -> str:
     base = {1: "trace_literal", 2: "trace_brute", 3: "trace_brute_lds", 4: "trace_bundle", 5: "trace_bundle_cull",
             6: "trace_bundle_bvh"}
     if kernel == 7:
         return f"void hrt::trace_bundle_cull_lds<{block}>(hrt::TraceParams)"
+    if kernel == 8:
+        return "hrt::trace_bundle_bvh_lds(hrt::TraceParams)"
     return f"hrt::{base.get(kernel, '?')}(hrt::TraceParams)"
 
 
 KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull", 6: "bundle_bvh",
-                7: "bundle_cull_lds"}
+                7: "bundle_cull_lds", 8: "bundle_bvh_lds"}
 DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounce_iters", "bounce_considered",
               "bounce_survivors", "bounce_lanes", "bvh_visits", "bvh_prim_tests", "bvh_band_tests", "primary_cycles", "bounce_cycles",
               "shade_cycles", "bounce_stage2", "bounce_front", "bvh_trips",
@@ -96,9 +98,9 @@ SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh
 EXPORTED_SYMBOLS = (
     "hrt_abi_version", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate",
     "hrt_read_image", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
-    "hrt_get_diagnostics", "hrt_get_scene_info",
+    "hrt_get_diagnostics", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
     "hrt_stream", "hrt_last_error",
-    "hrt_host_create_rays", "hrt_host_view_matrix", "hrt_host_transform_meshes",
+    "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
     "hrt_obj_load", "hrt_obj_num_meshes", "hrt_obj_mesh", "hrt_obj_free",
 )
 
@@ -139,6 +141,10 @@ def load() -> ctypes.CDLL:
         "hrt_reset_stats": (c_int32, [P]),
         "hrt_get_diagnostics": (c_int32, [P, P, c_uint32]),
         "hrt_get_scene_info": (c_int32, [P, P, c_uint32]),
+        "hrt_generate_rays": (c_int32, [P, c_float, c_float, POINTER(c_float), POINTER(c_float)]),
+        "hrt_read_rays": (c_int32, [P, P, c_uint32]),
+        "hrt_host_ray_grid": (c_uint32, [c_uint32, c_uint32, c_float, c_float, POINTER(c_float), POINTER(c_float),
+                                         POINTER(c_float), POINTER(c_float), POINTER(c_float)]),
         "hrt_set_option": (c_int32, [P, c_uint32, c_int64]),
         "hrt_stream": (c_void_p, [P]),
         "hrt_last_error": (c_char_p, [P]),

@@ -15,6 +15,7 @@
 
 #include "hip_raytrace.h"
 #include "hrt_bvh.h"
+#include "hrt_host.h"
 #include "hrt_kernels.h"
 
 static_assert(sizeof(hrt_material) == 48, "std430 RayTracingMaterial");
@@ -56,6 +57,8 @@ struct hrt_context {
   float4* accum32 = nullptr;
   void* scratch = nullptr;  // format conversion for hrt_read_image
   unsigned long long* counters = nullptr;
+  uint32_t* tile_counter = nullptr;  // persistent LDS kernels' work counter
+  uint32_t num_cus = 0;
   uint32_t* cam_meta = nullptr;   // bundle variants: cam_start[n_meshes], cam_count[n_meshes]
   uint32_t cam_capacity = 0;      // sum of mesh lengths
   float4* cam_tris = nullptr;     // compacted camera-facing records (64 B each)
@@ -64,8 +67,11 @@ struct hrt_context {
   float4* bvh_prims = nullptr;
   float4* bvh_irregular = nullptr;
   uint32_t* bvh_band_off = nullptr;
+  uint32_t* bvh_entries = nullptr;
+  uint32_t* bvh_keybase = nullptr;
   float4* bvh_band = nullptr;
   uint32_t bvh_info[HRT_NUM_SCENE_INFO] = {};  // hrt_get_scene_info
+  float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f;
   uint32_t bvh_leaf = 4;
 
   int variant = 0;
@@ -195,6 +201,13 @@ extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_
   if ((e = hipMalloc(&ctx->scratch, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(scratch)"));
   if ((e = hipMalloc((void**)&ctx->counters, kNumCounters * sizeof(unsigned long long))) != hipSuccess)
     return bail(hip_fail(ctx, e, "hipMalloc(counters)"));
+  if ((e = hipMalloc((void**)&ctx->tile_counter, 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(tiles)"));
+  {
+    int cus = 0;
+    if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device)) != hipSuccess)
+      return bail(hip_fail(ctx, e, "hipDeviceGetAttribute(CUs)"));
+    ctx->num_cus = cus > 0 ? (uint32_t)cus : 1u;
+  }
   if ((e = hipMemsetAsync(ctx->counters, 0, kNumCounters * sizeof(unsigned long long), ctx->stream)) != hipSuccess)
     return bail(hip_fail(ctx, e, "hipMemset(counters)"));
   // Fresh images read as the cleared state (0,0,0,1) until the first dispatch writes them.
@@ -254,8 +267,10 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
                                     uint32_t n_spheres, const hrt_triangle* tris, uint32_t n_tris,
                                     const hrt_mesh* meshes, uint32_t n_meshes) {
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
-  if ((uint64_t)n_rays != (uint64_t)ctx->width * ctx->height || !rays)
-    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_set_scene: need width*height rays");
+  const bool keep_rays = !rays && n_rays == 0 && ctx->rays && ctx->n_rays == (uint64_t)ctx->width * ctx->height;
+  if (!keep_rays && ((uint64_t)n_rays != (uint64_t)ctx->width * ctx->height || !rays))
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT,
+                "hrt_set_scene: need width*height rays (or NULL after hrt_generate_rays)");
   if ((n_spheres && !spheres) || (n_tris && !tris) || (n_meshes && !meshes))
     return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_set_scene: null record array with nonzero count");
   for (uint32_t m = 0; m < n_meshes; ++m) {
@@ -266,7 +281,9 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
   static_assert(sizeof(float4) == sizeof(hrt_ray), "ray record");
-  if ((st = upload(ctx, ctx->rays, reinterpret_cast<const float4*>(rays), n_rays, "rays")) != HRT_OK) return st;
+  if (!keep_rays &&
+      (st = upload(ctx, ctx->rays, reinterpret_cast<const float4*>(rays), n_rays, "rays")) != HRT_OK)
+    return st;
   if ((st = upload(ctx, ctx->spheres, spheres, n_spheres, "spheres")) != HRT_OK) return st;
   if ((st = upload(ctx, ctx->tris, tris, n_tris, "triangles")) != HRT_OK) return st;
   if ((st = upload(ctx, ctx->meshes, meshes, n_meshes, "meshes")) != HRT_OK) return st;
@@ -289,6 +306,8 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   free_dev(ctx->bvh_irregular);
   free_dev(ctx->bvh_band_off);
   free_dev(ctx->bvh_band);
+  free_dev(ctx->bvh_entries);
+  free_dev(ctx->bvh_keybase);
   if (built) {
     auto up = [&](auto*& dst, const auto& v) -> hrt_status {
       const size_t bytes = v.size() * sizeof(v[0]);
@@ -301,15 +320,19 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
     if ((st = up(ctx->bvh_irregular, bvh.irregular)) != HRT_OK) return st;
     if ((st = up(ctx->bvh_band_off, bvh.band_off)) != HRT_OK) return st;
     if ((st = up(ctx->bvh_band, bvh.band_list)) != HRT_OK) return st;  // 16 B entries
+    if ((st = up(ctx->bvh_entries, bvh.entries)) != HRT_OK) return st;
+    if ((st = up(ctx->bvh_keybase, bvh.key_base)) != HRT_OK) return st;
   }
   ctx->bvh_info[0] = bvh.n_nodes;
   ctx->bvh_info[1] = bvh.n_prims;
   ctx->bvh_info[2] = bvh.n_irregular;
   ctx->bvh_info[3] = bvh.n_never;
   ctx->bvh_info[4] = built ? 1u : 0u;
+  ctx->bvh_abs_coef = bvh.abs_coef;
+  ctx->bvh_rel_t = bvh.rel_t;
   ctx->bvh_info[5] = (uint32_t)(bvh.band_list.size() / 4);
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
-  ctx->n_rays = n_rays;
+  if (!keep_rays) ctx->n_rays = n_rays;
   ctx->n_spheres = n_spheres;
   ctx->n_tris = n_tris;
   ctx->n_meshes = n_meshes;
@@ -353,12 +376,20 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.cam_tris = ctx->cam_tris;
   p.cam_cull = ctx->cam_cull;
   p.sec_batch = ctx->sec_batch;
+  p.tile_counter = ctx->tile_counter;
+  p.num_cus = ctx->num_cus;
   p.bvh_nodes = ctx->bvh_info[4] ? ctx->bvh_nodes : nullptr;
   p.bvh_prims = ctx->bvh_prims;
   p.bvh_irregular = ctx->bvh_irregular;
   p.bvh_band_off = ctx->bvh_band_off;
   p.bvh_band = ctx->bvh_band;
+  p.bvh_entries = ctx->bvh_entries;
+  p.bvh_keybase = ctx->bvh_keybase;
+  p.bvh_n_prims = ctx->bvh_info[1];
+  p.bvh_n_meshes = ctx->n_meshes;
   p.bvh_n_nodes = ctx->bvh_info[0];
+  p.bvh_abs_coef = ctx->bvh_abs_coef;
+  p.bvh_rel_t = ctx->bvh_rel_t;
   p.bvh_n_irregular = ctx->bvh_info[2];
   const int variant = ctx->variant;
 
@@ -477,6 +508,34 @@ extern "C" hrt_status hrt_get_diagnostics(hrt_context* ctx, uint64_t* out, uint3
   return HRT_OK;
 }
 
+extern "C" hrt_status hrt_generate_rays(hrt_context* ctx, float camera_focal_length, float viewport_height,
+                                        const float up[3], float* default_jitter) {
+  if (!ctx || !up) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  float first[3], px[3], py[3];
+  const uint32_t n = hrt_host_ray_grid(ctx->width, ctx->height, camera_focal_length, viewport_height, up, first, px,
+                                       py, default_jitter);
+  const size_t want = (size_t)ctx->width * ctx->height;
+  if (!ctx->rays || ctx->n_rays != want) {
+    free_dev(ctx->rays);
+    HRT_HIP(ctx, hipMalloc((void**)&ctx->rays, (want ? want : 1) * sizeof(float4)));
+  }
+  if (n) HRT_HIP(ctx, hrt::launch_make_rays(ctx->rays, ctx->width, ctx->height, first, px, py, ctx->stream));
+  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->n_rays = (uint32_t)want;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_read_rays(hrt_context* ctx, hrt_ray* out, uint32_t n) {
+  if (!ctx || (!out && n) || (uint64_t)n > ctx->n_rays || !ctx->rays)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_rays: no rays or n too large");
+  hrt_status st = hrt_synchronize(ctx);
+  if (st != HRT_OK) return st;
+  if (n) HRT_HIP(ctx, hipMemcpy(out, ctx->rays, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
+  return HRT_OK;
+}
+
 extern "C" hrt_status hrt_get_scene_info(hrt_context* ctx, uint32_t* out, uint32_t count) {
   if (!ctx || !out || count > HRT_NUM_SCENE_INFO) return HRT_ERR_INVALID_ARGUMENT;
   for (uint32_t i = 0; i < count; ++i) out[i] = ctx->bvh_info[i];
@@ -499,8 +558,8 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   switch (key) {
     case HRT_OPT_KERNEL_VARIANT:
-      if (value < HRT_KERNEL_AUTO || value > HRT_KERNEL_BUNDLE_CULL_LDS)
-        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be an hrt_kernel value (0..7)");
+      if (value < HRT_KERNEL_AUTO || value > HRT_KERNEL_BUNDLE_BVH_LDS)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be an hrt_kernel value (0..8)");
       ctx->variant = (int)value;
       return HRT_OK;
     case HRT_OPT_COUNTERS:

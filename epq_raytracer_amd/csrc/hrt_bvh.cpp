@@ -80,6 +80,7 @@ struct Builder {
                            t.edge_two[0], t.edge_two[1], t.edge_two[2], bits_f(en.index),
                            t.normal[0], t.normal[1], t.normal[2], 0.0f};
     out.prims.insert(out.prims.end(), rec, rec + 16);
+    out.entries.push_back(en.index | (en.mesh << 26));
   }
 
   void build(uint32_t b, uint32_t n, const hrt_triangle* tris) {
@@ -171,15 +172,24 @@ struct Builder {
       if (mid <= b || mid >= b + n) mid = b + n / 2;  // coincident centroids: split the range
     }
 
+    // box margin for a lane whose origin is within R of every scene vertex: mg = a + b R, from
+    // eta = 6e + (1.01 rho + 3.2e + 18.4e G R) / (tau_g - rho - 4e-7) (DESIGN.md "BVH cull"), plus
+    // 4e x the box's largest coordinate for the kernel's rounding of lo - mg / hi + mg
+    const double eps = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)kBandTau - rho - 4e-7);
+    const double coord = std::max({std::fabs(box.lo.x), std::fabs(box.lo.y), std::fabs(box.lo.z),
+                                   std::fabs(box.hi.x), std::fabs(box.hi.y), std::fabs(box.hi.z)});
+    const double a_m = 2.02 * ext * (6 * eps + (1.01 * rho + 3.2 * eps) * inv_tp) + 4 * eps * coord;
+    const double b_m = 2.02 * ext * 18.4 * eps * g * inv_tp;
+    out.rho_max = std::max(out.rho_max, rho);
     float* r = &out.nodes[(size_t)node * 16];
     r[0] = round_down(box.lo.x);
     r[1] = round_down(box.lo.y);
     r[2] = round_down(box.lo.z);
-    r[3] = round_up(ext * (1.0 + 1e-12));
+    r[3] = round_up(a_m * (1.0 + 1e-6));
     r[4] = round_up(box.hi.x);
     r[5] = round_up(box.hi.y);
     r[6] = round_up(box.hi.z);
-    r[7] = round_up(g * (1.0 + 1e-9));
+    r[7] = round_up(b_m * (1.0 + 1e-6));
     r[8] = (float)axis.x;
     r[9] = (float)axis.y;
     r[10] = (float)axis.z;
@@ -305,12 +315,13 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
   if (n_meshes > kBvhMaxMeshes) return false;
   uint64_t total = 0;
   for (uint32_t m = 0; m < n_meshes; ++m) total += meshes[m].len;
-  if (total > kBvhMaxEntries) return false;
+  if (total > kBvhMaxEntries || n_tris >= (1u << 26)) return false;
   leaf_size = std::max(1u, std::min(leaf_size, kBvhMaxLeafCount));
   std::vector<Entry> entries;
   entries.reserve(total);
   uint32_t key = 1;
   for (uint32_t m = 0; m < n_meshes; ++m) {
+    out.key_base.push_back(key - meshes[m].first_index);  // key of (m, first_index + k) = key + k
     for (uint32_t k = 0; k < meshes[m].len; ++k, ++key) {
       const uint32_t i = meshes[m].first_index + k;
       if (i >= n_tris) continue;  // hrt_set_scene validated the ranges
@@ -361,6 +372,10 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
     bld.build(0, (uint32_t)entries.size(), tris);
   }
   build_band_lists(out);
+  // t-slack of the box test for a lane at distance <= R: abs = abs_coef R, rel
+  const double e = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)kBandTau - out.rho_max - 4e-7);
+  out.abs_coef = round_up(2.1 * (4.2 * e + out.rho_max) * inv_tp * (1.0 + 1e-6));
+  out.rel_t = round_up((2.1 * (3.2 * e + out.rho_max) * inv_tp + 4 * e) * (1.0 + 1e-6));
   return true;
 }
 

@@ -17,9 +17,9 @@ namespace hrt {
 
 // 16 floats per node:
 //   [0..2]  box lo (vertices a, a+e1, a+e2 of every triangle below, rounded outward)
-//   [3]     tri_ext: max over those triangles of their largest per-axis extent
+//   [3]     margin a: the box grows by a + b R for a lane whose origin is within R of every vertex
 //   [4..6]  box hi
-//   [7]     G = max |e|max / |n|   (1 / length; conditioning of the barycentric numerators)
+//   [7]     margin b (from tri_ext = the largest per-axis triangle extent below and G = max |e|/|n|)
 //   [8..10] normal-cone axis c (unit)
 //   [11]    cos(phi)   (phi >= angle(c, n_i / |n_i|) for every triangle; (0, 1) = no cone)
 //   [12]    sin(phi)
@@ -36,9 +36,13 @@ struct BvhHost {
   std::vector<float> nodes;
   std::vector<float> prims;      // leaf-ordered regular triangles
   std::vector<float> irregular;  // entries the analysis does not cover: tested for every bounce ray
+  std::vector<uint32_t> entries;    // per leaf prim: triangle index | mesh << 26
+  std::vector<uint32_t> key_base;   // per mesh: scan key of (m, i) = key_base[m] + i (mod 2^32)
   std::vector<uint32_t> band_off;   // 6 kDirRes^2 + 1 offsets into band_list
   std::vector<uint32_t> band_list;  // 4 words per entry: n^ (3 floats, rounded), prim index
   uint32_t n_nodes = 0, n_prims = 0, n_irregular = 0, n_never = 0;  // never = zero normal (dn == 0)
+  double rho_max = 0.0;
+  float abs_coef = 0.0f, rel_t = 0.0f;  // box-test t-slack: [-abs_coef R, best (1 + rel_t) + abs_coef R]
 };
 
 constexpr float kBandTau = 3e-3f;
@@ -52,7 +56,8 @@ constexpr uint32_t kBvhMaxLeafCount = 16;  // leaf count lives in bits 27..31 of
 constexpr uint64_t kBvhMaxEntries = 1u << 18;
 
 // Builds the hierarchy over every (mesh, triangle) entry of the scene.  Returns false (and leaves
-// `out` empty) when the scene has more than kBvhMaxMeshes meshes or kBvhMaxEntries entries.
+// `out` empty) when the scene has more than kBvhMaxMeshes meshes, kBvhMaxEntries entries or 2^26
+// triangles.
 bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
                uint32_t leaf_size, BvhHost& out);
 

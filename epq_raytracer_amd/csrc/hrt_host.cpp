@@ -32,9 +32,9 @@ constexpr float kF32Max = 3.40282347e+38f;
 
 }  // namespace
 
-extern "C" uint32_t hrt_host_create_rays(uint32_t width, uint32_t height, float camera_focal_length,
-                                         float viewport_height, const float up[3], hrt_ray* out,
-                                         float* default_jitter) {
+extern "C" uint32_t hrt_host_ray_grid(uint32_t width, uint32_t height, float camera_focal_length,
+                                      float viewport_height, const float up[3], float first[3], float px[3],
+                                      float py[3], float* default_jitter) {
   // zero length protection, src/raytrace_pipeline.rs:298-303
   if (width == 0 || height == 0) {
     if (default_jitter) *default_jitter = 0.0f;
@@ -45,23 +45,38 @@ extern "C" uint32_t hrt_host_create_rays(uint32_t width, uint32_t height, float 
   const V3 vx = normalised(cross(V3{up[0], up[1], up[2]}, X));                 // :309
   const V3 vy = normalised(cross(vx, X));                                      // :310
   const V3 ul = (V3{0.0f, 0.0f, 0.0f} + X * camera_focal_length) - (vx * vw + vy * viewport_height) * 0.5f;  // :311
-  const V3 px = vx * vw / (float)width;                                        // :313
-  const V3 py = vy * viewport_height / (float)height;                          // :314
-  const V3 first = ul + (px + py) * 0.5f;                                      // :316
-  if (out) {
-    for (uint32_t y = 0; y < height; ++y) {                                    // :319-326
-      for (uint32_t x = 0; x < width; ++x) {
-        const V3 r = first + px * (float)x + py * (float)y;
-        hrt_ray& o = out[(size_t)y * width + x];
-        o.sample_centre[0] = r.x;
-        o.sample_centre[1] = r.y;
-        o.sample_centre[2] = r.z;
-        o.sample_centre[3] = 1.0f;  // extend(); unused by the kernel
-      }
+  const V3 dx = vx * vw / (float)width;                                        // :313
+  const V3 dy = vy * viewport_height / (float)height;                          // :314
+  const V3 f = ul + (dx + dy) * 0.5f;                                          // :316
+  const float fv[3] = {f.x, f.y, f.z}, xv[3] = {dx.x, dx.y, dx.z}, yv[3] = {dy.x, dy.y, dy.z};
+  for (int k = 0; k < 3; ++k) {
+    if (first) first[k] = fv[k];
+    if (px) px[k] = xv[k];
+    if (py) py[k] = yv[k];
+  }
+  if (default_jitter) *default_jitter = fmax_rs(magnitude(dx), magnitude(dy)) * 0.5f;  // :337
+  return width * height;
+}
+
+extern "C" uint32_t hrt_host_create_rays(uint32_t width, uint32_t height, float camera_focal_length,
+                                         float viewport_height, const float up[3], hrt_ray* out,
+                                         float* default_jitter) {
+  float f[3], dx[3], dy[3];
+  const uint32_t n = hrt_host_ray_grid(width, height, camera_focal_length, viewport_height, up, f, dx, dy,
+                                       default_jitter);
+  if (n == 0 || !out) return n;
+  const V3 first{f[0], f[1], f[2]}, px{dx[0], dx[1], dx[2]}, py{dy[0], dy[1], dy[2]};
+  for (uint32_t y = 0; y < height; ++y) {                                      // :319-326
+    for (uint32_t x = 0; x < width; ++x) {
+      const V3 r = first + px * (float)x + py * (float)y;
+      hrt_ray& o = out[(size_t)y * width + x];
+      o.sample_centre[0] = r.x;
+      o.sample_centre[1] = r.y;
+      o.sample_centre[2] = r.z;
+      o.sample_centre[3] = 1.0f;  // extend(); unused by the kernel
     }
   }
-  if (default_jitter) *default_jitter = fmax_rs(magnitude(px), magnitude(py)) * 0.5f;  // :337
-  return width * height;
+  return n;
 }
 
 extern "C" void hrt_host_view_matrix(const float direction[3], const float up[3], float out[16]) {

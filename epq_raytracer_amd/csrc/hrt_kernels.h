@@ -28,19 +28,27 @@ struct TraceParams {
   float4* cam_tris;              // 4 float4 per record: (ao, num_t) (e1, index bits) (e2, -) (n, -)
   float4* cam_cull;              // 5 float4 per record: bundle-cull linear forms + margins
   uint32_t sec_batch;            // bounce segments run once this many lanes of a wave wait (1..64)
-  uint32_t lds_tile_cap;         // BUNDLE_CULL_LDS: primary-list entries per wave (set by launch_trace)
+  uint32_t lds_tile_cap;         // LDS variants: primary-list entries per wave (set by launch_trace)
+  uint32_t* tile_counter;        // LDS variants (persistent): next 8x8 tile, reset by launch_trace
+  uint32_t num_cus;              // compute units of the device (persistent grid size)
   // BUNDLE_BVH: bounce-segment hierarchy built by hrt_set_scene (hrt_bvh.h records); nullptr = none.
   const float4* bvh_nodes;       // 4 float4 per node, preorder with escape indices
   const float4* bvh_prims;       // 4 float4 per leaf triangle
   const float4* bvh_irregular;   // 4 float4 per entry outside the analysis (tested for every ray)
   const uint32_t* bvh_band_off;  // kDirCells + 1 offsets: grazing-band prims per direction cell
   const float4* bvh_band;        // (n^, prim index bits) per entry
-  uint32_t bvh_n_nodes, bvh_n_irregular;
+  const uint32_t* bvh_entries;   // per leaf prim: triangle index | mesh << 26 (BUNDLE_BVH_LDS)
+  const uint32_t* bvh_keybase;   // per mesh: key = keybase[m] + triangle index
+  uint32_t bvh_n_nodes, bvh_n_irregular, bvh_n_prims, bvh_n_meshes;
+  float bvh_abs_coef, bvh_rel_t;  // box-test t-slack (hrt_bvh.h)
 };
 
 // Launches the trace kernel(s); *ran / *block receive the resolved hrt_kernel and workgroup size.
 hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, int* ran, int* block);
 int resolve_variant(const TraceParams& p, int variant);  // the kernel an HRT_KERNEL_* request runs
+// Ray centres (first + px * x) + py * y for every pixel of a width x height image (hrt_generate_rays).
+hipError_t launch_make_rays(float4* rays, uint32_t width, uint32_t height, const float first[3], const float px[3],
+                            const float py[3], hipStream_t stream);
 hipError_t launch_clear(uint32_t* img8, float4* img32, size_t npix, hipStream_t stream);
 hipError_t launch_accumulate(uint32_t* cur8, const uint32_t* new8, float4* cur32, const float4* new32, size_t npix,
                              uint32_t frame, hipStream_t stream);

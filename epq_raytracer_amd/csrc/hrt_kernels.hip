@@ -826,17 +826,16 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
 //            (e = 2^-24, R >= |o - a| over the node, G and rho from the node record).
 // So a node is skipped when its normal cone is entirely back-facing, or when the ray segment
 // t in [-abs, best (1 + rel) + abs] misses the node box grown by 2 eta tri_ext (plus coordinate
-// rounding), tau = max(kBandTau, -max over the cone of d.n^): no triangle below can then be
-// accepted with dist <= best except band triangles, which the band list covers.  Equal distances are
+// rounding) at tau = kBandTau and R = the lane origin's distance to the farthest scene-box corner
+// (node margin a + b R and abs = abs_coef R precomputed by hrt_bvh.cpp): no triangle below can then
+// be accepted with dist <= best except band triangles, which the band list covers.  Equal distances are
 // resolved by the scan key (first in the reference's mesh/index order wins).
-constexpr float kEps = 5.9604644775390625e-08f;  // 2^-24
 
-__device__ __forceinline__ void bvh_prim_test(const float4* __restrict__ pr, uint32_t k, unsigned long long mask, f3 o,
-                                              f3 d, Closest& c, uint32_t& bkey, float& best_k) {
-  const float4 A = pr[4 * k], B = pr[4 * k + 1];
-  const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
-  if (!((mask >> m) & 1ull)) return;  // mesh failed its (quirky) AABB test for this lane
-  const float4 N = pr[4 * k + 3];
+// The exact per-lane test of one BVH entry (triangle idx of mesh m, scan key), raytracing.glsl:213-241
+// with the running closest (ties: lower key).
+__device__ __forceinline__ void bvh_tri_test(const float4& A, const float4& B, const float4& C, const float4& N,
+                                             uint32_t key, uint32_t idx, uint32_t m, f3 o, f3 d, Closest& c,
+                                             uint32_t& bkey, float& best_k) {
   const f3 n = mk(N.x, N.y, N.z);
   const f3 ao = o - mk(A.x, A.y, A.z);
   TriPre q;
@@ -844,7 +843,6 @@ __device__ __forceinline__ void bvh_prim_test(const float4* __restrict__ pr, uin
   if (!(q.num_t > 0.0f)) return;
   const float dn = dot(d, n);
   if (!(dn < 0.0f)) return;
-  const float4 C = pr[4 * k + 2];
   const f3 dao = cross(ao, d);
   q.num_u = dot(mk(C.x, C.y, C.z), dao);
   q.num_v = dot(mk(B.x, B.y, B.z), dao);
@@ -855,45 +853,78 @@ __device__ __forceinline__ void bvh_prim_test(const float4* __restrict__ pr, uin
   const float u = q.num_u * inv_det;
   const float v = -q.num_v * inv_det;
   const float w = 1.0f - u - v;
-  const uint32_t key = __builtin_bit_cast(uint32_t, A.w);
   if (!(dist < 0.0f) && !(u < 0.0f) && !(v < 0.0f) && !(w < 0.0f) && dist > 0.001f &&
       (dist < c.t || (dist == c.t && key < bkey))) {
-    c = Closest{dist, 2, __builtin_bit_cast(uint32_t, C.w), m};
+    c = Closest{dist, 2, idx, m};
     bkey = key;
     best_k = dist * kOnePlus;
   }
 }
 
+// BVH entry k from 64 B records (a, key) (e1, mesh) (e2, index) (n, -) (leaf prims, irregular list).
+__device__ __forceinline__ void bvh_prim_test(const float4* __restrict__ pr, uint32_t k, unsigned long long mask, f3 o,
+                                              f3 d, Closest& c, uint32_t& bkey, float& best_k) {
+  const float4 A = pr[4 * k], B = pr[4 * k + 1];
+  const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
+  if (!((mask >> m) & 1ull)) return;  // mesh failed its (quirky) AABB test for this lane
+  const float4 C = pr[4 * k + 2], N = pr[4 * k + 3];
+  bvh_tri_test(A, B, C, N, __builtin_bit_cast(uint32_t, A.w), __builtin_bit_cast(uint32_t, C.w), m, o, d, c, bkey,
+               best_k);
+}
+
+// Hierarchy sources: node k (4 float4) and leaf / band entry k.
+struct BvhGlobal {
+  const float4* __restrict__ nodes;
+  const float4* __restrict__ prims;
+  __device__ __forceinline__ void node(uint32_t k, float4& N0, float4& N1, float4& N2, float4& N3) const {
+    N0 = nodes[4 * k];
+    N1 = nodes[4 * k + 1];
+    N2 = nodes[4 * k + 2];
+    N3 = nodes[4 * k + 3];
+  }
+  __device__ __forceinline__ void prim(uint32_t k, unsigned long long mask, f3 o, f3 d, Closest& c, uint32_t& bkey,
+                                       float& best_k) const {
+    bvh_prim_test(prims, k, mask, o, d, c, bkey, best_k);
+  }
+};
+struct BvhLds {  // nodes and the triangle image in LDS; entry k = triangle | mesh << 26, key = kbase[m] + triangle
+  const float4* nodes;
+  const float4* tris;
+  const uint32_t* entries;
+  const uint32_t* kbase;
+  __device__ __forceinline__ void node(uint32_t k, float4& N0, float4& N1, float4& N2, float4& N3) const {
+    N0 = nodes[4 * k];
+    N1 = nodes[4 * k + 1];
+    N2 = nodes[4 * k + 2];
+    N3 = nodes[4 * k + 3];
+  }
+  __device__ __forceinline__ void prim(uint32_t k, unsigned long long mask, f3 o, f3 d, Closest& c, uint32_t& bkey,
+                                       float& best_k) const {
+    const uint32_t e = entries[k], idx = e & 0x03FFFFFFu, m = e >> 26;
+    if (!((mask >> m) & 1ull)) return;
+    float4 A, B, C, N;
+    LdsTris{tris}(idx, A, B, C, N);
+    bvh_tri_test(A, B, C, N, kbase[m] + idx, idx, m, o, d, c, bkey, best_k);
+  }
+};
+
 // true when the node may hold a triangle the reference accepts for (o, d) with dist <= best.
+// R >= |o - a| for every vertex of the scene (the lane's origin to the root box's farthest corner),
+// abs = abs_coef R: the per-lane part of the node test, computed once per bounce segment.
 __device__ __forceinline__ bool bvh_node_visit(const float4& N0, const float4& N1, const float4& N2, const float4& N3,
-                                               f3 o, f3 d, f3 inv, float best) {
+                                               f3 o, f3 d, f3 inv, float R, float abs_t, float t_hi) {
   const float x = N2.x * d.x + N2.y * d.y + N2.z * d.z;  // cos(angle(d, axis)) within 2e-6
   const float xa = fmaxf(fabsf(x) - 2e-6f, 0.0f);
   const float s_up = __builtin_sqrtf(fmaxf(1.0f - xa * xa, 0.0f)) + 1e-6f;
-  const float xc = x * N2.w, ss = s_up * N3.x;
-  if (xc - ss - 1e-6f > 1e-5f) return false;  // back: every dn > 0
-  const float tau = fmaxf(kBandTau, -(xc + ss + 1e-6f));
-  const float rho = N3.y;  // <= 1e-4 (hrt_bvh.cpp: larger goes to the irregular list)
-  const float inv_tp = 1.02f / (tau - rho - 4e-7f);
-  const f3 lo = mk(N0.x, N0.y, N0.z), hi = mk(N1.x, N1.y, N1.z);
-  const f3 ctr = (lo + hi) * 0.5f, half = (hi - lo) * 0.5f;
-  const f3 oc = o - ctr;
-  const float R = (__builtin_sqrtf(dot(oc, oc)) + __builtin_sqrtf(dot(half, half))) * 1.0001f;
-  const float abs_t = 2.1f * (4.2f * kEps + rho) * R * inv_tp;
-  const float rel_t = 2.1f * (3.2f * kEps + rho) * inv_tp + 4.0f * kEps;
-  const float eta = 6.0f * kEps + (1.01f * rho + 3.2f * kEps + 18.4f * kEps * N1.w * R) * inv_tp;
-  const float coord = fmaxf(fmaxf(fabsf(ctr.x), fabsf(ctr.y)), fabsf(ctr.z)) +
-                      fmaxf(fmaxf(half.x, half.y), half.z);
-  const float mg = 2.02f * eta * N0.w + 4.0f * kEps * coord;
-  const float t_hi = best * (1.0f + rel_t) + abs_t;
-  const float tx0 = ((lo.x - mg) - o.x) * inv.x, tx1 = ((hi.x + mg) - o.x) * inv.x;
-  const float ty0 = ((lo.y - mg) - o.y) * inv.y, ty1 = ((hi.y + mg) - o.y) * inv.y;
-  const float tz0 = ((lo.z - mg) - o.z) * inv.z, tz1 = ((hi.z + mg) - o.z) * inv.z;
+  if (x * N2.w - s_up * N3.x - 1e-6f > 1e-5f) return false;  // back: every dn > 0
+  const float mg = N0.w + N1.w * R;
+  const float tx0 = ((N0.x - mg) - o.x) * inv.x, tx1 = ((N1.x + mg) - o.x) * inv.x;
+  const float ty0 = ((N0.y - mg) - o.y) * inv.y, ty1 = ((N1.y + mg) - o.y) * inv.y;
+  const float tz0 = ((N0.z - mg) - o.z) * inv.z, tz1 = ((N1.z + mg) - o.z) * inv.z;
   const float tn = fmaxf(fmaxf(-abs_t, fminf(tx0, tx1)), fmaxf(fminf(ty0, ty1), fminf(tz0, tz1)));
   const float tf = fminf(fminf(t_hi, fmaxf(tx0, tx1)), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
   return !((tn - fabsf(tn) * 1e-6f) > (tf + fabsf(tf) * 1e-6f));  // NaN -> visit
 }
-
 // Cube-map cell of a direction (hrt_bvh.cpp face_dir is the inverse): face = 2 * major axis +
 // (component < 0), (u, v) = the two minor components over the major one's magnitude.
 __device__ __forceinline__ uint32_t dir_cell(f3 d) {
@@ -921,8 +952,9 @@ __device__ __forceinline__ uint32_t dir_cell(f3 d) {
 
 // Bounce segments through the hierarchy.  Called with ALL 64 lanes active (spheres and the
 // irregular list are wave-uniform loops; the traversal and the band list are per lane).
-__device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const TraceParams& P, bool sec, f3 o, f3 d,
-                                                     uint32_t& tests, Closest& c, Diag& dg) {
+template <class Bvh>
+__device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const TraceParams& P, const Bvh& bvh, bool sec,
+                                                     f3 o, f3 d, uint32_t& tests, Closest& c, Diag& dg) {
   const hrt_push_constants& pc = P.pc;
   spheres_first(sc, pc, sec, o, d, c);
   unsigned long long mask = 0ull;
@@ -940,7 +972,15 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
   for (uint32_t k = 0; k < P.bvh_n_irregular; ++k)
     if (sec) bvh_prim_test(P.bvh_irregular, k, mask, o, d, c, bkey, best_k);
   const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-  const float4* __restrict__ nodes = P.bvh_nodes;
+  float R = 0.0f;
+  if (P.bvh_n_nodes) {  // farthest root-box corner from the origin, rounded up
+    float4 R0, R1, R2, R3;
+    bvh.node(0, R0, R1, R2, R3);
+    const float fx = fmaxf(fabsf(o.x - R0.x), fabsf(R1.x - o.x)), fy = fmaxf(fabsf(o.y - R0.y), fabsf(R1.y - o.y));
+    const float fz = fmaxf(fabsf(o.z - R0.z), fabsf(R1.z - o.z));
+    R = __builtin_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0001f;
+  }
+  const float abs_t = P.bvh_abs_coef * R;
   const uint32_t end = P.bvh_n_nodes;
   uint32_t node = (sec && mask) ? 0u : end;
   uint32_t visits = 0, prim_tests = 0, band_tests = 0;
@@ -958,7 +998,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
       for (int j = 0; j < 4; ++j) {
         const float dn = d.x * qs[j].x + d.y * qs[j].y + d.z * qs[j].z;
         if (dn > lo && dn < hi) {
-          bvh_prim_test(P.bvh_prims, __builtin_bit_cast(uint32_t, qs[j].w), mask, o, d, c, bkey, best_k);
+          bvh.prim(__builtin_bit_cast(uint32_t, qs[j].w), mask, o, d, c, bkey, best_k);
           ++band_tests;
         }
       }
@@ -967,7 +1007,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
       const float4 q = P.bvh_band[k];
       const float dn = d.x * q.x + d.y * q.y + d.z * q.z;
       if (dn > lo && dn < hi) {
-        bvh_prim_test(P.bvh_prims, __builtin_bit_cast(uint32_t, q.w), mask, o, d, c, bkey, best_k);
+        bvh.prim(__builtin_bit_cast(uint32_t, q.w), mask, o, d, c, bkey, best_k);
         ++band_tests;
       }
     }
@@ -975,16 +1015,18 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
   uint32_t trips = 0, leaf_trips = 0;  // wave-level loop iterations (diagnostics)
   while (node < end) {
     if (P.diag) ++trips;
-    const float4 N0 = nodes[4 * node], N1 = nodes[4 * node + 1], N2 = nodes[4 * node + 2], N3 = nodes[4 * node + 3];
+    float4 N0, N1, N2, N3;
+    bvh.node(node, N0, N1, N2, N3);
     const uint32_t info = __builtin_bit_cast(uint32_t, N3.z);
     const uint32_t esc = __builtin_bit_cast(uint32_t, N3.w);
-    const bool visit = bvh_node_visit(N0, N1, N2, N3, o, d, inv, c.t);
+    const float t_hi = c.t * (1.0f + P.bvh_rel_t) + abs_t;
+    const bool visit = bvh_node_visit(N0, N1, N2, N3, o, d, inv, R, abs_t, t_hi);
     const uint32_t count = info >> 27;
     ++visits;
     if (P.diag && __any(visit && count)) ++leaf_trips;
     if (visit && count) {
       const uint32_t first = info & 0x07FFFFFFu;
-      for (uint32_t k = first; k < first + count; ++k) bvh_prim_test(P.bvh_prims, k, mask, o, d, c, bkey, best_k);
+      for (uint32_t k = first; k < first + count; ++k) bvh.prim(k, mask, o, d, c, bkey, best_k);
       prim_tests += count;
     }
     node = (visit && !count) ? node + 1 : esc;
@@ -1006,9 +1048,10 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
 enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2 };
 
-template <int Bounce, class CullSrc>
+template <int Bounce, class CullSrc, class BvhSrc = BvhGlobal>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, uint32_t* tile_slice,
-                                                  uint32_t tile_cap, const CullSrc& csrc) {
+                                                  uint32_t tile_cap, const CullSrc& csrc,
+                                                  const BvhSrc& bsrc = BvhSrc{}) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
   const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
@@ -1072,7 +1115,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
       if constexpr (Bounce == kBounceBvh) {
-        world_hit_bounce_bvh(sc, P, sec, p.pos, p.dir, tests, c, dg);
+        world_hit_bounce_bvh(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
       } else if constexpr (Bounce == kBounceCull) {
         world_hit_bounce_cull(sc, P, csrc, sec, p.pos, p.dir, tests, c, dg);
       } else {
@@ -1152,30 +1195,75 @@ __global__ __launch_bounds__(256) void trace_bundle_bvh(TraceParams P) {
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
   trace_fused_split<kBounceBvh>(P, x, lr, tile_lds + (threadIdx.x >> 6) * kTileCap, kTileCap,
-                                CullGlobal{T, to_const(T)});
+                                CullGlobal{T, to_const(T)}, BvhGlobal{P.bvh_nodes, P.bvh_prims});
 }
 
-// BUNDLE_CULL with the triangles resident in LDS (bounce survivors are read at LDS rather than L2
-// latency).  Dynamic LDS: [n_tris x 48 B triangles][waves x tile_cap x 4 B primary lists].
-// Workgroups of BLOCK threads cover (BLOCK/64 waves) 8x8 tiles: 512 -> 32x16 pixels, 1024 -> 32x32.
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
+
+// Stage the triangle buffer into LDS in the BRUTE_LDS image (3 float4 per triangle).
+__device__ __forceinline__ void stage_tris(const TraceParams& P, float4* dst, uint32_t block) {
   const uint32_t n = P.n_tris;
-  for (uint32_t k = threadIdx.x; k < 3 * n; k += BLOCK) {
+  for (uint32_t k = threadIdx.x; k < 3 * n; k += block) {
     const uint32_t i = k / 3, part = k - 3 * i;
     const hrt_triangle& t = P.tris[i];
     float4 v;
     if (part == 0) v = make_float4(t.a[0], t.a[1], t.a[2], t.normal[0]);
     else if (part == 1) v = make_float4(t.normal[1], t.normal[2], t.edge_one[0], t.edge_one[1]);
     else v = make_float4(t.edge_one[2], t.edge_two[0], t.edge_two[1], t.edge_two[2]);
-    lds_tris[k] = v;
+    dst[k] = v;
   }
+}
+
+// Persistent tile loop of the LDS-resident variants: the workgroups stay resident (one or two per CU,
+// the scene staged once) and each wave takes 8x8 pixel tiles from a global counter until the image
+// is done, so no wave idles while a slower wave of its workgroup finishes.  Every wave leaves the
+// loop once the counter passes the tile count.
+template <class Body>
+__device__ __forceinline__ void tile_loop(const TraceParams& P, Body&& body) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t tiles_x = (P.pc.width + 7) / 8, tiles = tiles_x * ((P.local_rows + 7) / 8);
+  for (;;) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(P.tile_counter, 1u);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t >= tiles) break;
+    const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+    body(tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
+  }
+}
+
+// BUNDLE_CULL with the triangles resident in LDS (bounce survivors are read at LDS rather than L2
+// latency).  Dynamic LDS: [n_tris x 48 B triangles][waves x tile_cap x 4 B primary lists].
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
+  stage_tris(P, lds_tris, BLOCK);
   __syncthreads();
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t x = blockIdx.x * 32 + (wave & 3) * 8 + (lane & 7);
-  const uint32_t lr = blockIdx.y * (BLOCK / 32) + (wave >> 2) * 8 + (lane >> 3);
-  uint32_t* lists = reinterpret_cast<uint32_t*>(lds_tris + 3 * n);
-  trace_fused_split<kBounceCull>(P, x, lr, lists + wave * P.lds_tile_cap, P.lds_tile_cap, CullLds{lds_tris});
+  const uint32_t wave = threadIdx.x >> 6;
+  uint32_t* lists = reinterpret_cast<uint32_t*>(lds_tris + 3 * P.n_tris) + wave * P.lds_tile_cap;
+  tile_loop(P, [&](uint32_t x, uint32_t lr) {
+    trace_fused_split<kBounceCull>(P, x, lr, lists, P.lds_tile_cap, CullLds{lds_tris});
+  });
+}
+
+// BUNDLE_BVH with the hierarchy and the triangle image in LDS (persistent 1024-thread workgroups).
+// Dynamic LDS: [n_tris x 48 B triangles][nodes x 64 B][prims x 4 B entries][meshes x 4 B key bases]
+// [16 x lds_tile_cap x 4 B primary lists].
+__global__ __launch_bounds__(1024) void trace_bundle_bvh_lds(TraceParams P) {
+  const uint32_t n = P.n_tris, nn = P.bvh_n_nodes, np = P.bvh_n_prims, nm = P.bvh_n_meshes;
+  stage_tris(P, lds_tris, 1024);
+  float4* nodes = lds_tris + 3 * n;
+  for (uint32_t k = threadIdx.x; k < 4 * nn; k += 1024) nodes[k] = P.bvh_nodes[k];
+  uint32_t* entries = reinterpret_cast<uint32_t*>(nodes + 4 * nn);
+  for (uint32_t k = threadIdx.x; k < np; k += 1024) entries[k] = P.bvh_entries[k];
+  uint32_t* kbase = entries + np;
+  for (uint32_t k = threadIdx.x; k < nm; k += 1024) kbase[k] = P.bvh_keybase[k];
+  __syncthreads();
+  const uint32_t wave = threadIdx.x >> 6;
+  uint32_t* lists = kbase + nm + wave * P.lds_tile_cap;
+  const float4* T = reinterpret_cast<const float4*>(P.tris);
+  tile_loop(P, [&](uint32_t x, uint32_t lr) {
+    trace_fused_split<kBounceBvh>(P, x, lr, lists, P.lds_tile_cap, CullGlobal{T, to_const(T)},
+                                  BvhLds{nodes, lds_tris, entries, kbase});
+  });
 }
 
 // Per-frame prep for the bundle variants: one workgroup per mesh, order-preserving compaction of the
@@ -1238,6 +1326,19 @@ __global__ __launch_bounds__(256) void camera_lists(TraceParams P) {
     P.cam_start[m] = start;
     P.cam_count[m] = base_s;
   }
+}
+
+// ---- ray centres (create_ray_subbuffer's loop, src/raytrace_pipeline.rs:319-326) ------------------
+// (first + px * x) + py * y per component, each product and sum rounded as written (-ffp-contract=off):
+// the same bits as hrt_host_create_rays.
+__global__ __launch_bounds__(256) void make_rays(float4* rays, uint32_t width, uint32_t height, float fx, float fy,
+                                                 float fz, float pxx, float pxy, float pxz, float pyx, float pyy,
+                                                 float pyz) {
+  const uint32_t x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (x >= width || y >= height) return;
+  const float xf = (float)x, yf = (float)y;
+  rays[(size_t)y * width + x] = make_float4((fx + pxx * xf) + pyx * yf, (fy + pxy * xf) + pyy * yf,
+                                            (fz + pxz * xf) + pyz * yf, 1.0f);
 }
 
 // ---- init clear (raytracing.glsl:363-366) and image_combiner.glsl (:22-43) ----------------------
@@ -1307,6 +1408,15 @@ constexpr uint32_t kAutoBvhTris = 4096;   // BUNDLE_BVH from this many (profiles
 // BUNDLE_CULL_LDS workgroup size for a scene of n triangles (0 = does not fit) and the per-wave
 // primary-list capacity left over: two 512-thread workgroups per CU when twice the footprint fits the
 // 160 KiB, else one of 1024.
+// BUNDLE_BVH_LDS footprint check: triangles + nodes + entries + key bases + 16 primary lists.
+bool bvh_lds_fits(const TraceParams& p, uint32_t* cap) {
+  const size_t fixed = (size_t)p.n_tris * 48 + (size_t)p.bvh_n_nodes * 64 + (size_t)p.bvh_n_prims * 4 +
+                       (size_t)p.bvh_n_meshes * 4;
+  if (!p.bvh_nodes || !p.bvh_entries || fixed + 16 * 16 * 4 > kMaxLdsScene) return false;
+  if (cap) *cap = (uint32_t)std::min<size_t>(kTileCap, (kMaxLdsScene - fixed) / (16 * 4));
+  return true;
+}
+
 uint32_t lds_block(uint32_t n, uint32_t* cap) {
   constexpr size_t kMinCap = 16;
   const size_t tri = (size_t)n * 48;
@@ -1333,6 +1443,8 @@ int resolve_variant(const TraceParams& p, int variant) {
   if (variant == HRT_KERNEL_BRUTE_LDS && (size_t)p.n_tris * 48 > kMaxLdsScene) variant = HRT_KERNEL_BRUTE;
   if (variant == HRT_KERNEL_BUNDLE_BVH && (!p.bvh_nodes || p.pc.num_meshes > 64)) variant = HRT_KERNEL_BUNDLE_CULL;
   if (variant == HRT_KERNEL_BUNDLE_CULL_LDS && lds_block(p.n_tris, nullptr) == 0) variant = HRT_KERNEL_BUNDLE_CULL;
+  if (variant == HRT_KERNEL_BUNDLE_BVH_LDS && !bvh_lds_fits(p, nullptr)) variant = HRT_KERNEL_BUNDLE_BVH;
+  if (variant == HRT_KERNEL_BUNDLE_BVH_LDS && (!p.bvh_nodes || p.pc.num_meshes > 64)) variant = HRT_KERNEL_BUNDLE_CULL;
   if (p.pc.max_bounces < 0) variant = HRT_KERNEL_LITERAL;  // the fused loops assume >= 1 segment per path
   return variant;
 }
@@ -1346,6 +1458,8 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_bundle_cull_lds<512>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kMaxLdsScene / 2));
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_bundle_bvh_lds),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
   }
   variant = resolve_variant(p, variant);
@@ -1361,19 +1475,28 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       trace_brute_lds<<<g32, 1024, (size_t)p.n_tris * 48, stream>>>(p);
       break;
     }
+    case HRT_KERNEL_BUNDLE_BVH_LDS: {
+      if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      TraceParams q = p;
+      bvh_lds_fits(p, &q.lds_tile_cap);
+      const size_t lds = (size_t)p.n_tris * 48 + (size_t)p.bvh_n_nodes * 64 + (size_t)p.bvh_n_prims * 4 +
+                         (size_t)p.bvh_n_meshes * 4 + (size_t)16 * q.lds_tile_cap * 4;
+      if (hipError_t e = hipMemsetAsync(p.tile_counter, 0, 4, stream); e != hipSuccess) return e;
+      trace_bundle_bvh_lds<<<p.num_cus, 1024, lds, stream>>>(q);
+      *block_out = 1024;
+      break;
+    }
     case HRT_KERNEL_BUNDLE_CULL_LDS: {
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       TraceParams q = p;
       const uint32_t block = lds_block(p.n_tris, &q.lds_tile_cap);
       *block_out = (int)block;
       const size_t lds = (size_t)p.n_tris * 48 + (size_t)(block / 64) * q.lds_tile_cap * 4;
-      if (block == 512) {
-        const dim3 g((p.pc.width + 31) / 32, (p.local_rows + 15) / 16, 1);
-        trace_bundle_cull_lds<512><<<g, 512, lds, stream>>>(q);
-      } else {
-        const dim3 g((p.pc.width + 31) / 32, (p.local_rows + 31) / 32, 1);
-        trace_bundle_cull_lds<1024><<<g, 1024, lds, stream>>>(q);
-      }
+      if (hipError_t e = hipMemsetAsync(p.tile_counter, 0, 4, stream); e != hipSuccess) return e;
+      if (block == 512)
+        trace_bundle_cull_lds<512><<<2 * p.num_cus, 512, lds, stream>>>(q);
+      else
+        trace_bundle_cull_lds<1024><<<p.num_cus, 1024, lds, stream>>>(q);
       break;
     }
     case HRT_KERNEL_BUNDLE:
@@ -1391,6 +1514,15 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       trace_brute<<<grid, 256, 0, stream>>>(p);
       break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_make_rays(float4* rays, uint32_t width, uint32_t height, const float first[3], const float px[3],
+                            const float py[3], hipStream_t stream) {
+  if (width == 0 || height == 0) return hipSuccess;
+  const dim3 g((width + 15) / 16, (height + 15) / 16, 1);
+  make_rays<<<g, 256, 0, stream>>>(rays, width, height, first[0], first[1], first[2], px[0], px[1], px[2], py[0],
+                                   py[1], py[2]);
   return hipGetLastError();
 }
 

@@ -124,9 +124,26 @@ class HrtContext:
         _lib.check(st, where, self.handle)
 
     def set_scene(self, rays, spheres, tris, meshes):
-        self._check(self.lib.hrt_set_scene(self.handle, _lib.ptr(rays), len(rays), _lib.ptr(spheres), len(spheres),
-                                           _lib.ptr(tris), len(tris), _lib.ptr(meshes), len(meshes)),
+        """rays=None keeps the context's rays (hrt_generate_rays or an earlier set_scene)."""
+        n_rays = 0 if rays is None else len(rays)
+        self._check(self.lib.hrt_set_scene(self.handle, None if rays is None else _lib.ptr(rays), n_rays,
+                                           _lib.ptr(spheres), len(spheres), _lib.ptr(tris), len(tris),
+                                           _lib.ptr(meshes), len(meshes)),
                     "hrt_set_scene")
+
+    def generate_rays(self, camera_focal_length: float, viewport_height: float, up) -> float:
+        """Ray centres on the device (hrt_generate_rays); returns the default jitter."""
+        u = (ctypes.c_float * 3)(*[float(np.float32(v)) for v in up])
+        jit = ctypes.c_float()
+        self._check(self.lib.hrt_generate_rays(self.handle, float(np.float32(camera_focal_length)),
+                                               float(np.float32(viewport_height)), u, ctypes.byref(jit)),
+                    "hrt_generate_rays")
+        return jit.value
+
+    def read_rays(self) -> np.ndarray:
+        out = np.empty(self.width * self.height, dtype=_lib.RAY_DTYPE)
+        self._check(self.lib.hrt_read_rays(self.handle, _lib.ptr(out), len(out)), "hrt_read_rays")
+        return out
 
     def trace(self, pc: _lib.PushConstants):
         self._check(self.lib.hrt_trace(self.handle, ctypes.byref(pc)), "hrt_trace")

@@ -162,8 +162,10 @@ typedef enum hrt_kernel {
   HRT_KERNEL_BUNDLE_BVH = 6,  /* BUNDLE + per-lane BVH traversal of bounce rays (hierarchy built by
                                  hrt_set_scene; falls back to BUNDLE_CULL above 64 meshes or 2^18
                                  mesh triangles) */
-  HRT_KERNEL_BUNDLE_CULL_LDS = 7 /* BUNDLE_CULL with the triangle buffer resident in LDS (512/1024-thread
+  HRT_KERNEL_BUNDLE_CULL_LDS = 7, /* BUNDLE_CULL with the triangle buffer resident in LDS (512/1024-thread
                                     workgroups; falls back to BUNDLE_CULL above ~3,300 triangles) */
+  HRT_KERNEL_BUNDLE_BVH_LDS = 8   /* BUNDLE_BVH with the hierarchy and triangles in LDS (1024-thread
+                                    workgroups; falls back to BUNDLE_BVH when they exceed 160 KiB) */
 } hrt_kernel;
 
 /* Option keys for hrt_set_option. */
@@ -219,7 +221,8 @@ uint32_t hrt_abi_version(void);
 hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_ctx);
 void hrt_destroy(hrt_context* ctx);
 
-/* Upload the scene.  rays: n_rays == width*height records indexed by global pixel id x + y*W.
+/* Upload the scene.  rays: n_rays == width*height records indexed by global pixel id x + y*W
+ * (or NULL / 0 to keep the rays of an earlier hrt_generate_rays / hrt_set_scene).
  * spheres/tris/meshes may be NULL when their count is 0 (the reference's "null object" records are
  * not needed).  Every mesh range must lie inside [0, n_tri).  Copies before returning. */
 hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint32_t n_rays, const hrt_sphere* spheres,
@@ -245,6 +248,15 @@ hrt_status hrt_get_diagnostics(hrt_context* ctx, uint64_t* out, uint32_t count);
 /* Extension (no reference counterpart): out[i] = hrt_scene_info i for i < count, from the last
  * hrt_set_scene. */
 hrt_status hrt_get_scene_info(hrt_context* ctx, uint32_t* out, uint32_t count);
+
+/* On-device ray centres: fills the context's ray buffer with exactly the records
+ * hrt_host_create_rays would produce (create_ray_subbuffer, src/raytrace_pipeline.rs:289-338) for
+ * the context's width x height, without the host array or its upload.  A later hrt_set_scene may then
+ * pass rays == NULL, n_rays == 0 to keep them.  default_jitter (may be NULL) receives :337's value. */
+hrt_status hrt_generate_rays(hrt_context* ctx, float camera_focal_length, float viewport_height, const float up[3],
+                             float* default_jitter);
+/* Copies n (<= width*height) ray records of the context to host memory (verification). */
+hrt_status hrt_read_rays(hrt_context* ctx, hrt_ray* out, uint32_t n);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
 /* HIP stream the context's work is ordered on (hipStream_t), for callers that interoperate. */

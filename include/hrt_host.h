@@ -6,6 +6,8 @@
  * under the documented assumptions on rust_maths.
  *
  *   hrt_host_create_rays       create_ray_subbuffer   src/raytrace_pipeline.rs:289-338
+ *   hrt_host_ray_grid          its per-image constants (:298-316, :337); hrt_generate_rays
+ *                              (hip_raytrace.h) evaluates the per-pixel loop :319-326 on the device
  *   hrt_host_view_matrix       get_view_matrix        src/raytrace_pipeline.rs:269-285
  *   hrt_host_transform_meshes  transform_meshes       src/raytrace_pipeline.rs:377-428
  *                              (+ create_mesh_subbuffer :363-374 first_index bookkeeping)
@@ -27,6 +29,11 @@ extern "C" {
  * (0 for a zero-sized image, like the reference's zero-length protection :298-303). */
 uint32_t hrt_host_create_rays(uint32_t width, uint32_t height, float camera_focal_length, float viewport_height,
                               const float up[3], hrt_ray* out, float* default_jitter);
+
+/* The grid behind hrt_host_create_rays: ray (x, y) = (first + px * x) + py * y, each operation
+ * rounded as written.  Any output pointer may be NULL.  Returns width*height (0: zero-sized). */
+uint32_t hrt_host_ray_grid(uint32_t width, uint32_t height, float camera_focal_length, float viewport_height,
+                           const float up[3], float first[3], float px[3], float py[3], float* default_jitter);
 
 /* Column-major mat4 for push_constants.cam_alignment_mat: columns = normalised direction,
  * new_y, new_z (so mat3(M) * (1,0,0) = direction / |direction|), 4th column (0,0,0,1). */

@@ -39,7 +39,7 @@ def test_library_loads_and_reports_abi():
 def test_code_object_targets_gfx950():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob  # the fat binary carries a gfx950 code object
-    for k in (b"trace_literal", b"trace_brute", b"trace_brute_lds", b"trace_bundle", b"trace_bundle_cull", b"trace_bundle_bvh", b"trace_bundle_cull_lds", b"camera_lists"):
+    for k in (b"trace_literal", b"trace_brute", b"trace_brute_lds", b"trace_bundle", b"trace_bundle_cull", b"trace_bundle_bvh", b"trace_bundle_cull_lds", b"trace_bundle_bvh_lds", b"camera_lists"):
         assert k in blob, k
 
 

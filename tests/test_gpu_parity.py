@@ -14,7 +14,7 @@ from helpers import E, SceneCase, _lib, mismatch_report
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [0, 1]  # auto (tuned), literal
-ALL_VARIANTS = list(range(8))  # every hrt_kernel value (hrt_set_option HRT_OPT_KERNEL_VARIANT)
+ALL_VARIANTS = list(range(9))  # every hrt_kernel value (hrt_set_option HRT_OPT_KERNEL_VARIANT)
 
 CONFIGS = [
     # (scene, size, spp, bounces, rng_offset)
@@ -310,6 +310,34 @@ def test_bvh_leaf_sizes(leaf):
     assert (s.segments, s.tri_tests) == (seg, tt)
 
 
+@pytest.mark.parametrize("size", [(1, 1), (37, 23), (1920, 1080)])
+@pytest.mark.parametrize("up", [(0.0, 1.0, 0.0), (0.1, 0.9, 0.2)])
+def test_device_rays_match_host(size, up):
+    """hrt_generate_rays (SURVEY.md 8(f) on-device ray centres) == hrt_host_create_rays, byte for byte."""
+    ctx = E.HrtContext(size, device=0)
+    jit = ctx.generate_rays(1.0, 2.0, up)
+    got = ctx.read_rays()
+    ctx.close()
+    ref, n, jit2 = E.create_rays(size, 1.0, 2.0, up)
+    assert np.float32(jit) == np.float32(jit2)
+    np.testing.assert_array_equal(got.view(np.uint32), ref[:n].view(np.uint32))
+
+
+def test_trace_with_device_rays():
+    case = SceneCase("island", (96, 64), 4, 8)
+    ref, _, seg, tt = case.oracle()
+    ctx = E.HrtContext(case.size, device=0)
+    s = case.settings
+    ctx.generate_rays(s.camera_focal_length, s.viewport_height, s.up)
+    ctx.set_scene(None, case.spheres, case.tris, case.meshes)
+    ctx.trace(case.push())
+    img = ctx.read(_lib.IMG_TRACE)
+    st = ctx.stats()
+    ctx.close()
+    assert np.array_equal(img, ref), mismatch_report(img, ref)
+    assert (st.segments, st.tri_tests) == (seg, tt)
+
+
 def test_errors_fail_loudly():
     case = SceneCase("box", (32, 32), 1, 1)
     ctx = E.HrtContext((32, 32), device=0)
@@ -331,6 +359,10 @@ def test_errors_fail_loudly():
     with pytest.raises(_lib.HrtError, match="INVALID"):
         ctx.read_into(_lib.IMG_TRACE, _lib.FMT_RGBA8, np.zeros(4, np.uint8).ctypes.data, 4)
     ctx.close()
+    fresh = E.HrtContext((32, 32), device=0)
+    with pytest.raises(_lib.HrtError, match="INVALID"):  # no rays yet: NULL is not "keep"
+        fresh.set_scene(None, case.spheres, case.tris, case.meshes)
+    fresh.close()
 
 
 # ---- full size (1920x1080, 64 spp, 8 bounces: the headline workload) ------------------------

@@ -25,6 +25,26 @@ def test_create_rays_matches_oracle(size, up):
     np.testing.assert_array_equal(rays["sample_centre"][:n].view(np.uint32), ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("size", [(1, 1), (37, 23), (1920, 1080)])
+@pytest.mark.parametrize("up", [(0.0, 1.0, 0.0), (0.1, 0.9, 0.2)])
+def test_ray_grid_reproduces_create_rays(size, up):
+    """hrt_host_ray_grid's (first, px, py): (first + px*x) + py*y in binary32, each operation rounded
+    as written (what the device's make_rays evaluates), gives create_rays' records bit for bit."""
+    import ctypes
+    lib = _lib.load()
+    f3 = lambda v=(0.0, 0.0, 0.0): (ctypes.c_float * 3)(*v)
+    first, px, py, upc, jit = f3(), f3(), f3(), f3(up), ctypes.c_float()
+    n = lib.hrt_host_ray_grid(size[0], size[1], 1.0, 2.0, upc, first, px, py, ctypes.byref(jit))
+    rays, n2, jit2 = E.create_rays(size, 1.0, 2.0, up)
+    assert n == n2 and np.float32(jit.value) == np.float32(jit2)
+    f, a, b = (np.array(list(v), np.float32) for v in (first, px, py))
+    xs = np.arange(size[0], dtype=np.float32)[None, :, None]
+    ys = np.arange(size[1], dtype=np.float32)[:, None, None]
+    grid = (f + a * xs) + b * ys  # numpy float32: each op correctly rounded, no contraction
+    np.testing.assert_array_equal(grid.reshape(-1, 3).view(np.uint32),
+                                  rays["sample_centre"][:n, :3].view(np.uint32))
+
+
 def test_create_rays_geometry():
     # up=(0,1,0): viewport_x = (0,0,-1), viewport_y = (0,-1,0): row 0 is the top (SURVEY.md 8(a) A-18)
     rays, n, jit = E.create_rays((4, 2), 1.0, 2.0, (0, 1, 0))

@@ -44,7 +44,7 @@ def main():
         ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
         ctx.trace(pc)
         ref = ctx.read(_lib.IMG_TRACE)
-    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v in (0, 4, 5, 6, 7) else [a.sec_batch[0]])]
+    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v in (0, 4, 5, 6, 7, 8) else [a.sec_batch[0]])]
     res = {vs: [] for vs in combos}
     stats = {}
     same = {}
@@ -61,7 +61,7 @@ def main():
                 same[(v, sb)] = None if ref is None else bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
     if a.diag:
         for v in a.variants:
-            if v in (0, 4, 5, 6, 7):
+            if v in (0, 4, 5, 6, 7, 8):
                 ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
                 ctx.set_option(_lib.OPT_COUNTERS, 2)
                 ctx.reset_stats()
