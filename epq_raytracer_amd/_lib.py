@@ -76,14 +76,14 @@ OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2,
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
 KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS, KERNEL_BUNDLE_BVH_LDS = 6, 7, 8
 # kernel symbol (as rocprofv3 names it) of a resolved hrt_kernel + workgroup size
-def kernel_symbol(kernel: int, block: int) -> str:
-    base = {1: "trace_literal", 2: "trace_brute", 3: "trace_brute_lds", 4: "trace_bundle", 5: "trace_bundle_cull",
-            6: "trace_bundle_bvh"}
+def kernel_symbol(kernel: int, block: int, diag: bool = False) -> str:
+    d = "true" if diag else "false"
+    if kernel in (1, 2, 3):
+        return "hrt::" + {1: "trace_literal", 2: "trace_brute", 3: "trace_brute_lds"}[kernel] + "(hrt::TraceParams)"
     if kernel == 7:
-        return f"void hrt::trace_bundle_cull_lds<{block}>(hrt::TraceParams)"
-    if kernel == 8:
-        return "hrt::trace_bundle_bvh_lds(hrt::TraceParams)"
-    return f"hrt::{base.get(kernel, '?')}(hrt::TraceParams)"
+        return f"void hrt::trace_bundle_cull_lds<{block}, {d}>(hrt::TraceParams)"
+    name = {4: "trace_bundle", 5: "trace_bundle_cull", 6: "trace_bundle_bvh", 8: "trace_bundle_bvh_lds"}.get(kernel, "?")
+    return f"void hrt::{name}<{d}>(hrt::TraceParams)"
 
 
 KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull", 6: "bundle_bvh",

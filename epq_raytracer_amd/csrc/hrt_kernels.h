@@ -28,7 +28,6 @@ struct TraceParams {
   float4* cam_tris;              // 4 float4 per record: (ao, num_t) (e1, index bits) (e2, -) (n, -)
   float4* cam_cull;              // 5 float4 per record: bundle-cull linear forms + margins
   uint32_t sec_batch;            // bounce segments run once this many lanes of a wave wait (1..64)
-  uint32_t lds_tile_cap;         // LDS variants: primary-list entries per wave (set by launch_trace)
   uint32_t* tile_counter;        // LDS variants (persistent): next 8x8 tile, reset by launch_trace
   uint32_t num_cus;              // compute units of the device (persistent grid size)
   // BUNDLE_BVH: bounce-segment hierarchy built by hrt_set_scene (hrt_bvh.h records); nullptr = none.

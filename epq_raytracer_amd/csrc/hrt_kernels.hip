@@ -570,11 +570,12 @@ __device__ __forceinline__ void primary_exact(const kfloat* ct, uint32_t k, floa
 // through the farthest of X's 8 corner directions contains them all (a cap under 90 degrees is
 // convex), widened by 1e-5 in cosine for rounding.  The bundle cull against that cap runs ONCE per
 // wave; its survivors (camera-list index | mesh << 27, in buffer order) are the only triangles any
-// primary segment of the wave can hit, so each primary iteration tests just those.
-constexpr uint32_t kTileCap = 256;  // list entries per wave (LDS); more -> per-iteration cull
+// primary segment of the wave can hit, so each primary iteration tests just those.  The list lives
+// in one VGPR (entry i in lane i, read back with v_readlane): no LDS traffic on the primary path.
+constexpr uint32_t kTileCap = 64;  // list entries per wave; more -> per-iteration cull
 
 struct TileList {
-  const uint32_t* e;  // this wave's slice of the block's LDS list
+  uint32_t v;  // lane i: entry i
   uint32_t n;
   bool ok;
 };
@@ -614,26 +615,27 @@ __device__ __forceinline__ bool bundle_keep(const float4* __restrict__ cr, uint3
 }
 
 // Builds the wave's list (all 64 lanes active; the caller synchronises before reading it).
-__device__ __forceinline__ TileList build_tile_list(const TraceParams& P, uint32_t* slice, uint32_t cap, bool active,
-                                                   f3 centre) {
+__device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool active, f3 centre) {
   const hrt_push_constants& pc = P.pc;
-  TileList t{slice, 0u, false};
+  TileList t{0u, 0u, false};
   if (pc.num_meshes > 32 || !__any(active)) return t;
   bool ok;
   const Bundle b = tile_bundle(pc, active, centre, ok);
   if (!ok) return t;
   const uint32_t lane = threadIdx.x & 63;
-  const unsigned long long below = (1ull << lane) - 1ull;
   for (int m = 0; m < pc.num_meshes; ++m) {
     const uint32_t k0 = P.cam_start[m], k1 = k0 + P.cam_count[m];
     for (uint32_t base = k0; base < k1; base += 64) {
       const uint32_t k = base + lane;
       const bool keep = k < k1 && bundle_keep(P.cam_cull, k, b);
-      const unsigned long long mask = __ballot(keep);
-      const uint32_t cnt = (uint32_t)__popcll(mask);
-      if (t.n + cnt > cap) return t;  // ok stays false: per-iteration cull
-      if (keep) slice[t.n + (uint32_t)__popcll(mask & below)] = k | ((uint32_t)m << 27);
-      t.n += cnt;
+      unsigned long long mask = __ballot(keep);
+      if (t.n + (uint32_t)__popcll(mask) > kTileCap) return t;  // ok stays false: per-iteration cull
+      while (mask) {  // few survivors: append each to the next lane
+        const uint32_t e = (base + (uint32_t)__builtin_ctzll(mask)) | ((uint32_t)m << 27);
+        mask &= mask - 1ull;
+        t.v = lane == t.n ? e : t.v;
+        ++t.n;
+      }
     }
   }
   t.ok = true;
@@ -658,7 +660,7 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
   float best_k = c.t * kOnePlus;
   const kfloat* ct = to_const(P.cam_tris);
   for (uint32_t i = 0; i < tl.n; ++i) {
-    const uint32_t e = __builtin_amdgcn_readfirstlane(tl.e[i]);
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
     const bool pass = (pass_mask >> m) & 1u;
     if (!__any(pass)) continue;
@@ -669,6 +671,7 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
 }
 
 // Primary segments of the lanes with prim == true.  Called with ALL 64 lanes of the wave active.
+template <bool D>
 __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TraceParams& P, bool prim, f3 o, f3 d,
                                                  uint32_t& tests, Closest& c, Diag& dg) {
   const hrt_push_constants& pc = P.pc;
@@ -696,7 +699,7 @@ __device__ __forceinline__ void world_hit_bundle(const Scene& sc, const TracePar
         keep = !rej;
       }
       unsigned long long mask = __ballot(keep);
-      if (P.diag) {
+      if (D && P.diag) {
         dg.prim_considered += min(64u, k1 - base);
         dg.prim_survivors += (uint32_t)__popcll(mask);
       }
@@ -749,7 +752,7 @@ struct CullLds {  // LDS image, 3 float4 per triangle: (a, n.x) (n.yz, e1.xy) (e
 //       lane has dn >= 0: rejected.
 // Lane j bounds triangle base+j; survivors (buffer order) get the exact per-lane two-stage test.
 // Called with ALL 64 lanes active.
-template <class Src>
+template <bool D, class Src>
 __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const TraceParams& P, const Src& src, bool sec,
                                                       f3 o, f3 d, uint32_t& tests, Closest& c, Diag& dg) {
   const hrt_push_constants& pc = P.pc;
@@ -787,7 +790,7 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
         keep = !(s1 | r1);
       }
       unsigned long long mask = __ballot(keep);
-      if (P.diag) {
+      if (D && P.diag) {
         dg.sec_considered += min(64u, k1 - base);
         dg.sec_survivors += (uint32_t)__popcll(mask);
       }
@@ -797,7 +800,7 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
         mask &= mask - 1ull;
         float4 A, B, C, N;
         src.uniform(kk, A, B, C, N);
-        if (P.diag && pass) {  // how far the two-stage test gets for this survivor
+        if (D && P.diag && pass) {  // how far the two-stage test gets for this survivor
           const f3 ao = o - mk(A.x, A.y, A.z);
           const bool s2 = dot(ao, mk(N.x, N.y, N.z)) > 0.0f;
           dg.sec_stage2 += __any(s2) ? 1u : 0u;
@@ -952,7 +955,7 @@ __device__ __forceinline__ uint32_t dir_cell(f3 d) {
 
 // Bounce segments through the hierarchy.  Called with ALL 64 lanes active (spheres and the
 // irregular list are wave-uniform loops; the traversal and the band list are per lane).
-template <class Bvh>
+template <bool D, class Bvh>
 __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const TraceParams& P, const Bvh& bvh, bool sec,
                                                      f3 o, f3 d, uint32_t& tests, Closest& c, Diag& dg) {
   const hrt_push_constants& pc = P.pc;
@@ -1014,7 +1017,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
   }
   uint32_t trips = 0, leaf_trips = 0;  // wave-level loop iterations (diagnostics)
   while (node < end) {
-    if (P.diag) ++trips;
+    if (D && P.diag) ++trips;
     float4 N0, N1, N2, N3;
     bvh.node(node, N0, N1, N2, N3);
     const uint32_t info = __builtin_bit_cast(uint32_t, N3.z);
@@ -1023,7 +1026,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
     const bool visit = bvh_node_visit(N0, N1, N2, N3, o, d, inv, R, abs_t, t_hi);
     const uint32_t count = info >> 27;
     ++visits;
-    if (P.diag && __any(visit && count)) ++leaf_trips;
+    if (D && P.diag && __any(visit && count)) ++leaf_trips;
     if (visit && count) {
       const uint32_t first = info & 0x07FFFFFFu;
       for (uint32_t k = first; k < first + count; ++k) bvh.prim(k, mask, o, d, c, bkey, best_k);
@@ -1031,7 +1034,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
     }
     node = (visit && !count) ? node + 1 : esc;
   }
-  if (P.diag) {
+  if (D && P.diag) {
     dg.bvh_visits += visits;
     dg.bvh_prims += prim_tests;
     dg.bvh_band += band_tests;
@@ -1048,9 +1051,8 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
 enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2 };
 
-template <int Bounce, class CullSrc, class BvhSrc = BvhGlobal>
-__device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, uint32_t* tile_slice,
-                                                  uint32_t tile_cap, const CullSrc& csrc,
+template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
+__device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, const CullSrc& csrc,
                                                   const BvhSrc& bsrc = BvhSrc{}) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
@@ -1067,11 +1069,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     centre = mk(rc.x, rc.y, rc.z);
   }
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
-  const TileList tl = build_tile_list(P, tile_slice, tile_cap, active, centre);
-  // The list is private to the wave and a wave's LDS accesses complete in order, so a wave-level
-  // barrier suffices (a __syncthreads() fence would also stop the compiler from scalarising the
-  // uniform scene loads that follow).
-  __builtin_amdgcn_wave_barrier();
+  const TileList tl = build_tile_list(P, active, centre);
   int sample = 0;
   Path p;
   p.bounce = pc.max_bounces + 1;
@@ -1095,7 +1093,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     const bool sec = waiting && run_sec;
     Closest c{kFltMax, 0, 0u, 0u};
     uint64_t t0 = 0, t1 = 0, t2 = 0;
-    if (P.diag) {
+    if (D && P.diag) {
       dg.prim_iters += any_prim ? 1u : 0u;
       dg.sec_iters += run_sec ? 1u : 0u;
       dg.sec_lanes += run_sec ? nwait : 0u;
@@ -1104,25 +1102,25 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (any_prim) {
       if (tl.ok) {
         world_hit_tile(sc, P, tl, prim, p.pos, p.dir, tests, c);
-        if (P.diag) {
+        if (D && P.diag) {
           dg.prim_considered += tl.n;
           dg.prim_survivors += tl.n;
         }
       } else {
-        world_hit_bundle(sc, P, prim, p.pos, p.dir, tests, c, dg);
+        world_hit_bundle<D>(sc, P, prim, p.pos, p.dir, tests, c, dg);
       }
     }
-    if (P.diag) t1 = __builtin_readcyclecounter();
+    if (D && P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
       if constexpr (Bounce == kBounceBvh) {
-        world_hit_bounce_bvh(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
+        world_hit_bounce_bvh<D>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
       } else if constexpr (Bounce == kBounceCull) {
-        world_hit_bounce_cull(sc, P, csrc, sec, p.pos, p.dir, tests, c, dg);
+        world_hit_bounce_cull<D>(sc, P, csrc, sec, p.pos, p.dir, tests, c, dg);
       } else {
         if (sec) c = world_hit_brute(sc, src, pc, p.pos, p.dir, tests);
       }
     }
-    if (P.diag) t2 = __builtin_readcyclecounter();
+    if (D && P.diag) t2 = __builtin_readcyclecounter();
     if (prim || sec) {
       ++segs;
       const bool ended = shade_step(sc, pc, p, c, state);
@@ -1132,7 +1130,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
         p.bounce = pc.max_bounces + 1;
       }
     }
-    if (P.diag) {
+    if (D && P.diag) {
       const uint64_t t3 = __builtin_readcyclecounter();
       dg.cyc_prim += t1 - t0;
       dg.cyc_sec += t2 - t1;
@@ -1167,35 +1165,32 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   }
 }
 
+template <bool D>
 __global__ __launch_bounds__(256) void trace_bundle(TraceParams P) {
-  __shared__ uint32_t tile_lds[4 * kTileCap];
   uint32_t x, lr;
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  trace_fused_split<kBounceBrute>(P, x, lr, tile_lds + (threadIdx.x >> 6) * kTileCap, kTileCap,
-                                  CullGlobal{T, to_const(T)});
+  trace_fused_split<kBounceBrute, D>(P, x, lr, CullGlobal{T, to_const(T)});
 }
 
 #ifndef HRT_CULL_WAVES
 #define HRT_CULL_WAVES 1
 #endif
+template <bool D>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HRT_CULL_WAVES))) void trace_bundle_cull(
     TraceParams P) {
-  __shared__ uint32_t tile_lds[4 * kTileCap];
   uint32_t x, lr;
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  trace_fused_split<kBounceCull>(P, x, lr, tile_lds + (threadIdx.x >> 6) * kTileCap, kTileCap,
-                                 CullGlobal{T, to_const(T)});
+  trace_fused_split<kBounceCull, D>(P, x, lr, CullGlobal{T, to_const(T)});
 }
 
+template <bool D>
 __global__ __launch_bounds__(256) void trace_bundle_bvh(TraceParams P) {
-  __shared__ uint32_t tile_lds[4 * kTileCap];
   uint32_t x, lr;
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  trace_fused_split<kBounceBvh>(P, x, lr, tile_lds + (threadIdx.x >> 6) * kTileCap, kTileCap,
-                                CullGlobal{T, to_const(T)}, BvhGlobal{P.bvh_nodes, P.bvh_prims});
+  trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhGlobal{P.bvh_nodes, P.bvh_prims});
 }
 
 
@@ -1232,21 +1227,17 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, Body&& body) {
 }
 
 // BUNDLE_CULL with the triangles resident in LDS (bounce survivors are read at LDS rather than L2
-// latency).  Dynamic LDS: [n_tris x 48 B triangles][waves x tile_cap x 4 B primary lists].
-template <int BLOCK>
+// latency).  Dynamic LDS: n_tris x 48 B triangles.
+template <int BLOCK, bool D>
 __global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
   stage_tris(P, lds_tris, BLOCK);
   __syncthreads();
-  const uint32_t wave = threadIdx.x >> 6;
-  uint32_t* lists = reinterpret_cast<uint32_t*>(lds_tris + 3 * P.n_tris) + wave * P.lds_tile_cap;
-  tile_loop(P, [&](uint32_t x, uint32_t lr) {
-    trace_fused_split<kBounceCull>(P, x, lr, lists, P.lds_tile_cap, CullLds{lds_tris});
-  });
+  tile_loop(P, [&](uint32_t x, uint32_t lr) { trace_fused_split<kBounceCull, D>(P, x, lr, CullLds{lds_tris}); });
 }
 
 // BUNDLE_BVH with the hierarchy and the triangle image in LDS (persistent 1024-thread workgroups).
-// Dynamic LDS: [n_tris x 48 B triangles][nodes x 64 B][prims x 4 B entries][meshes x 4 B key bases]
-// [16 x lds_tile_cap x 4 B primary lists].
+// Dynamic LDS: [n_tris x 48 B triangles][nodes x 64 B][prims x 4 B entries][meshes x 4 B key bases].
+template <bool D>
 __global__ __launch_bounds__(1024) void trace_bundle_bvh_lds(TraceParams P) {
   const uint32_t n = P.n_tris, nn = P.bvh_n_nodes, np = P.bvh_n_prims, nm = P.bvh_n_meshes;
   stage_tris(P, lds_tris, 1024);
@@ -1257,12 +1248,9 @@ __global__ __launch_bounds__(1024) void trace_bundle_bvh_lds(TraceParams P) {
   uint32_t* kbase = entries + np;
   for (uint32_t k = threadIdx.x; k < nm; k += 1024) kbase[k] = P.bvh_keybase[k];
   __syncthreads();
-  const uint32_t wave = threadIdx.x >> 6;
-  uint32_t* lists = kbase + nm + wave * P.lds_tile_cap;
   const float4* T = reinterpret_cast<const float4*>(P.tris);
   tile_loop(P, [&](uint32_t x, uint32_t lr) {
-    trace_fused_split<kBounceBvh>(P, x, lr, lists, P.lds_tile_cap, CullGlobal{T, to_const(T)},
-                                  BvhLds{nodes, lds_tris, entries, kbase});
+    trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhLds{nodes, lds_tris, entries, kbase});
   });
 }
 
@@ -1405,31 +1393,17 @@ constexpr size_t kMaxLdsScene = 160 * 1024;
 constexpr uint32_t kAutoCullTris = 256;   // BUNDLE_CULL from this many mesh triangles, BUNDLE below
 constexpr uint32_t kAutoBvhTris = 4096;   // BUNDLE_BVH from this many (profiles/r01d_bvh_scaling.log)
 
-// BUNDLE_CULL_LDS workgroup size for a scene of n triangles (0 = does not fit) and the per-wave
-// primary-list capacity left over: two 512-thread workgroups per CU when twice the footprint fits the
-// 160 KiB, else one of 1024.
-// BUNDLE_BVH_LDS footprint check: triangles + nodes + entries + key bases + 16 primary lists.
-bool bvh_lds_fits(const TraceParams& p, uint32_t* cap) {
-  const size_t fixed = (size_t)p.n_tris * 48 + (size_t)p.bvh_n_nodes * 64 + (size_t)p.bvh_n_prims * 4 +
-                       (size_t)p.bvh_n_meshes * 4;
-  if (!p.bvh_nodes || !p.bvh_entries || fixed + 16 * 16 * 4 > kMaxLdsScene) return false;
-  if (cap) *cap = (uint32_t)std::min<size_t>(kTileCap, (kMaxLdsScene - fixed) / (16 * 4));
-  return true;
+// BUNDLE_BVH_LDS footprint: triangles + nodes + entries + key bases.
+size_t bvh_lds_bytes(const TraceParams& p) {
+  return (size_t)p.n_tris * 48 + (size_t)p.bvh_n_nodes * 64 + (size_t)p.bvh_n_prims * 4 + (size_t)p.bvh_n_meshes * 4;
 }
+bool bvh_lds_fits(const TraceParams& p) { return p.bvh_nodes && p.bvh_entries && bvh_lds_bytes(p) <= kMaxLdsScene; }
 
-uint32_t lds_block(uint32_t n, uint32_t* cap) {
-  constexpr size_t kMinCap = 16;
+// BUNDLE_CULL_LDS workgroup size for a scene of n triangles (0 = does not fit): two 512-thread
+// workgroups per CU when twice the footprint fits the 160 KiB, else one of 1024.
+uint32_t lds_block(uint32_t n) {
   const size_t tri = (size_t)n * 48;
-  uint32_t block = 0, c = 0;
-  if (tri + 8 * kMinCap * 4 <= kMaxLdsScene / 2) {
-    block = 512;
-    c = (uint32_t)std::min<size_t>(kTileCap, (kMaxLdsScene / 2 - tri) / (8 * 4));
-  } else if (tri + 16 * kMinCap * 4 <= kMaxLdsScene) {
-    block = 1024;
-    c = (uint32_t)std::min<size_t>(kTileCap, (kMaxLdsScene - tri) / (16 * 4));
-  }
-  if (cap) *cap = c;
-  return block;
+  return tri <= kMaxLdsScene / 2 ? 512u : tri <= kMaxLdsScene ? 1024u : 0u;
 }
 
 int resolve_variant(const TraceParams& p, int variant) {
@@ -1437,13 +1411,13 @@ int resolve_variant(const TraceParams& p, int variant) {
     // profiles/r01g_*: island 21.4 (LDS) vs 23.7 ms, cave 112 vs 120 ms; BVH from ~4K triangles
     variant = p.cam_list_capacity >= kAutoBvhTris && p.bvh_nodes ? HRT_KERNEL_BUNDLE_BVH
               : p.cam_list_capacity < kAutoCullTris              ? HRT_KERNEL_BUNDLE
-              : lds_block(p.n_tris, nullptr) != 0                ? HRT_KERNEL_BUNDLE_CULL_LDS
+              : lds_block(p.n_tris) != 0                ? HRT_KERNEL_BUNDLE_CULL_LDS
                                                                  : HRT_KERNEL_BUNDLE_CULL;
   }
   if (variant == HRT_KERNEL_BRUTE_LDS && (size_t)p.n_tris * 48 > kMaxLdsScene) variant = HRT_KERNEL_BRUTE;
   if (variant == HRT_KERNEL_BUNDLE_BVH && (!p.bvh_nodes || p.pc.num_meshes > 64)) variant = HRT_KERNEL_BUNDLE_CULL;
-  if (variant == HRT_KERNEL_BUNDLE_CULL_LDS && lds_block(p.n_tris, nullptr) == 0) variant = HRT_KERNEL_BUNDLE_CULL;
-  if (variant == HRT_KERNEL_BUNDLE_BVH_LDS && !bvh_lds_fits(p, nullptr)) variant = HRT_KERNEL_BUNDLE_BVH;
+  if (variant == HRT_KERNEL_BUNDLE_CULL_LDS && lds_block(p.n_tris) == 0) variant = HRT_KERNEL_BUNDLE_CULL;
+  if (variant == HRT_KERNEL_BUNDLE_BVH_LDS && !bvh_lds_fits(p)) variant = HRT_KERNEL_BUNDLE_BVH;
   if (variant == HRT_KERNEL_BUNDLE_BVH_LDS && (!p.bvh_nodes || p.pc.num_meshes > 64)) variant = HRT_KERNEL_BUNDLE_CULL;
   if (p.pc.max_bounces < 0) variant = HRT_KERNEL_LITERAL;  // the fused loops assume >= 1 segment per path
   return variant;
@@ -1455,12 +1429,16 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
     lds_attr = true;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_brute_lds),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_bundle_cull_lds<512>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kMaxLdsScene / 2));
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_bundle_bvh_lds),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
+    const void* half_cu[] = {reinterpret_cast<const void*>(&trace_bundle_cull_lds<512, false>),
+                             reinterpret_cast<const void*>(&trace_bundle_cull_lds<512, true>)};
+    const void* whole_cu[] = {reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024, false>),
+                              reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024, true>),
+                              reinterpret_cast<const void*>(&trace_bundle_bvh_lds<false>),
+                              reinterpret_cast<const void*>(&trace_bundle_bvh_lds<true>)};
+    for (const void* f : half_cu)
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kMaxLdsScene / 2));
+    for (const void* f : whole_cu)
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
   }
   variant = resolve_variant(p, variant);
   *ran = variant;
@@ -1477,26 +1455,34 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
     }
     case HRT_KERNEL_BUNDLE_BVH_LDS: {
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
-      TraceParams q = p;
-      bvh_lds_fits(p, &q.lds_tile_cap);
-      const size_t lds = (size_t)p.n_tris * 48 + (size_t)p.bvh_n_nodes * 64 + (size_t)p.bvh_n_prims * 4 +
-                         (size_t)p.bvh_n_meshes * 4 + (size_t)16 * q.lds_tile_cap * 4;
+      const TraceParams& q = p;
+      const size_t lds = bvh_lds_bytes(p);
       if (hipError_t e = hipMemsetAsync(p.tile_counter, 0, 4, stream); e != hipSuccess) return e;
-      trace_bundle_bvh_lds<<<p.num_cus, 1024, lds, stream>>>(q);
+      if (p.diag)
+        trace_bundle_bvh_lds<true><<<p.num_cus, 1024, lds, stream>>>(q);
+      else
+        trace_bundle_bvh_lds<false><<<p.num_cus, 1024, lds, stream>>>(q);
       *block_out = 1024;
       break;
     }
     case HRT_KERNEL_BUNDLE_CULL_LDS: {
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
-      TraceParams q = p;
-      const uint32_t block = lds_block(p.n_tris, &q.lds_tile_cap);
+      const TraceParams& q = p;
+      const uint32_t block = lds_block(p.n_tris);
       *block_out = (int)block;
-      const size_t lds = (size_t)p.n_tris * 48 + (size_t)(block / 64) * q.lds_tile_cap * 4;
+      const size_t lds = (size_t)p.n_tris * 48;
       if (hipError_t e = hipMemsetAsync(p.tile_counter, 0, 4, stream); e != hipSuccess) return e;
-      if (block == 512)
-        trace_bundle_cull_lds<512><<<2 * p.num_cus, 512, lds, stream>>>(q);
-      else
-        trace_bundle_cull_lds<1024><<<p.num_cus, 1024, lds, stream>>>(q);
+      if (block == 512) {
+        if (p.diag)
+          trace_bundle_cull_lds<512, true><<<2 * p.num_cus, 512, lds, stream>>>(q);
+        else
+          trace_bundle_cull_lds<512, false><<<2 * p.num_cus, 512, lds, stream>>>(q);
+      } else {
+        if (p.diag)
+          trace_bundle_cull_lds<1024, true><<<p.num_cus, 1024, lds, stream>>>(q);
+        else
+          trace_bundle_cull_lds<1024, false><<<p.num_cus, 1024, lds, stream>>>(q);
+      }
       break;
     }
     case HRT_KERNEL_BUNDLE:
@@ -1504,11 +1490,13 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
     case HRT_KERNEL_BUNDLE_BVH:
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       if (variant == HRT_KERNEL_BUNDLE)
-        trace_bundle<<<grid, 256, 0, stream>>>(p);
+        p.diag ? trace_bundle<true><<<grid, 256, 0, stream>>>(p) : trace_bundle<false><<<grid, 256, 0, stream>>>(p);
       else if (variant == HRT_KERNEL_BUNDLE_CULL)
-        trace_bundle_cull<<<grid, 256, 0, stream>>>(p);
+        p.diag ? trace_bundle_cull<true><<<grid, 256, 0, stream>>>(p)
+               : trace_bundle_cull<false><<<grid, 256, 0, stream>>>(p);
       else
-        trace_bundle_bvh<<<grid, 256, 0, stream>>>(p);
+        p.diag ? trace_bundle_bvh<true><<<grid, 256, 0, stream>>>(p)
+               : trace_bundle_bvh<false><<<grid, 256, 0, stream>>>(p);
       break;
     default:
       trace_brute<<<grid, 256, 0, stream>>>(p);
