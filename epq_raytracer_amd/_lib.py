@@ -101,6 +101,7 @@ EXPORTED_SYMBOLS = (
     "hrt_get_diagnostics", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
     "hrt_stream", "hrt_last_error",
     "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
+    "hrt_debug_bvh_build",
     "hrt_obj_load", "hrt_obj_num_meshes", "hrt_obj_mesh", "hrt_obj_free",
 )
 
@@ -143,6 +144,8 @@ def load() -> ctypes.CDLL:
         "hrt_get_scene_info": (c_int32, [P, P, c_uint32]),
         "hrt_generate_rays": (c_int32, [P, c_float, c_float, POINTER(c_float), POINTER(c_float)]),
         "hrt_read_rays": (c_int32, [P, P, c_uint32]),
+        "hrt_debug_bvh_build": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, P, c_uint64, P, c_uint64, P,
+                                          c_uint64, P, c_uint64, P, c_uint64]),
         "hrt_host_ray_grid": (c_uint32, [c_uint32, c_uint32, c_float, c_float, POINTER(c_float), POINTER(c_float),
                                          POINTER(c_float), POINTER(c_float), POINTER(c_float)]),
         "hrt_set_option": (c_int32, [P, c_uint32, c_int64]),

@@ -380,3 +380,28 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
 }
 
 }  // namespace hrt
+
+// ---- host-only inspection (tests/test_bvh.py): build and copy out, no GPU involved ----------------
+extern "C" int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes,
+                                   uint32_t n_meshes, uint32_t leaf_size, uint32_t counts[6], float* nodes,
+                                   uint64_t nodes_cap, float* prims, uint64_t prims_cap, float* irregular,
+                                   uint64_t irregular_cap, uint32_t* band_off, uint64_t band_off_cap,
+                                   uint32_t* band_list, uint64_t band_list_cap) {
+  hrt::BvhHost b;
+  const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf_size, b);
+  counts[0] = b.n_nodes;
+  counts[1] = b.n_prims;
+  counts[2] = b.n_irregular;
+  counts[3] = b.n_never;
+  counts[4] = built ? 1u : 0u;
+  counts[5] = (uint32_t)(b.band_list.size() / 4);
+  if (!built) return 0;
+  auto copy = [](auto* dst, uint64_t cap, const auto& v) {
+    if (dst && cap >= v.size()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+    return !dst || cap >= v.size();
+  };
+  const bool ok = copy(nodes, nodes_cap, b.nodes) && copy(prims, prims_cap, b.prims) &&
+                  copy(irregular, irregular_cap, b.irregular) && copy(band_off, band_off_cap, b.band_off) &&
+                  copy(band_list, band_list_cap, b.band_list);
+  return ok ? 1 : -1;
+}

@@ -1,0 +1,237 @@
+"""The BUNDLE_BVH hierarchy as hrt_set_scene builds it (host C++, csrc/hrt_bvh.cpp), inspected on the
+CPU through hrt_debug_bvh_build: the structural facts the kernel's exact cull relies on (DESIGN.md
+"BVH cull").  The GPU parity tests check the frames; these check the invariants directly.
+
+* every (mesh, triangle) entry of the reference's scan sits in exactly one of: a leaf, the
+  irregular list (tested for every ray), or "never" (zero normal: raytracing.glsl:219 rejects it);
+* leaf records carry the entry's scan key (1 + position in mesh order, then index order);
+* the preorder / escape links visit every node once; child boxes nest in their parent's box and
+  every leaf triangle's vertices lie in its leaf box; the normal cone bounds every normal below;
+* grazing band: for random directions d, every regular triangle with d.n^ in
+  (-kBandTau - 1e-5, 2e-5) is in the band list of d's cube-map cell, the cell computed in binary32
+  exactly as the kernel's dir_cell does."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from helpers import E, SceneCase, _lib
+
+TAU_G = np.float32(3e-3)   # hrt_bvh.h kBandTau
+DIR_RES = 64               # hrt_bvh.h kDirRes
+CELLS = 6 * DIR_RES * DIR_RES
+
+
+def build(tris, meshes, leaf=4):
+    lib = _lib.load()
+    counts = (ctypes.c_uint32 * 6)()
+    P = ctypes.c_void_p
+    r = lib.hrt_debug_bvh_build(tris.ctypes.data, len(tris), meshes.ctypes.data, len(meshes), leaf, counts,
+                                None, 0, None, 0, None, 0, None, 0, None, 0)
+    nn, npr, nirr, nnever, built, nband = list(counts)
+    if not built:
+        return None
+    nodes = np.zeros(max(nn, 1) * 16, np.float32)
+    prims = np.zeros(max(npr, 1) * 16, np.float32)
+    irr = np.zeros(max(nirr, 1) * 16, np.float32)
+    boff = np.zeros(CELLS + 1, np.uint32)
+    band = np.zeros(max(nband, 1) * 4, np.uint32)
+    r = lib.hrt_debug_bvh_build(tris.ctypes.data, len(tris), meshes.ctypes.data, len(meshes), leaf, counts,
+                                P(nodes.ctypes.data), nodes.size, P(prims.ctypes.data), prims.size,
+                                P(irr.ctypes.data), irr.size, P(boff.ctypes.data), boff.size,
+                                P(band.ctypes.data), band.size)
+    assert r == 1
+    return dict(nodes=nodes[:nn * 16].reshape(nn, 16), prims=prims[:npr * 16].reshape(npr, 16),
+                irregular=irr[:nirr * 16].reshape(nirr, 16), never=nnever, band_off=boff,
+                band=band[:nband * 4].reshape(nband, 4))
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def ubits(x):
+    return int(np.array([x], np.float32).view(np.uint32)[0])
+
+
+def scan_entries(tris, meshes):
+    """(key, mesh, index) of every entry of the reference's scan, in scan order."""
+    out, key = [], 1
+    for m, mesh in enumerate(meshes):
+        for k in range(int(mesh["len"])):
+            out.append((key, m, int(mesh["first_index"]) + k))
+            key += 1
+    return out
+
+
+def adversarial_soup(seed=11):
+    rng = np.random.default_rng(seed)
+    v = []
+    for _ in range(150):  # slivers
+        a = rng.uniform(-3, 3, 3)
+        b = a + rng.uniform(-2, 2, 3)
+        v += [a, b, a + (b - a) * rng.uniform() + rng.normal(size=3) * 1e-6]
+    for _ in range(40):  # zero area
+        a = rng.uniform(-3, 3, 3)
+        v += [a, a, a + rng.uniform(-1, 1, 3)]
+    for _ in range(200):  # ordinary
+        a = rng.uniform(-5, 5, 3)
+        v += [a, a + rng.uniform(-1, 1, 3), a + rng.uniform(-1, 1, 3)]
+    v = np.array(v, np.float32)
+    mesh = E.Mesh(v, np.arange(len(v), dtype=np.uint32))
+    st = E.RayTracerSettings(num_samples=1, max_bounces=1, use_environment_lighting=True, mesh_data=[
+        E.RayTracingMesh(mesh, E.LambertianMaterial([0.5, 0.5, 0.5])),
+        E.RayTracingMesh(E.Mesh(v[::-1].copy(), np.arange(len(v), dtype=np.uint32)),
+                         E.LambertianMaterial([0.5, 0.5, 0.5]))])
+    return SceneCase(settings=st, camera=E.Camera([0, 0, -10], [0, 0, 1]), size=(8, 8))
+
+
+CASES = {
+    "island": lambda: SceneCase("island", (8, 8), 1, 1),
+    "cave": lambda: SceneCase("cave", (8, 8), 1, 1),
+    "box": lambda: SceneCase("box", (8, 8), 1, 1),
+    "soup": adversarial_soup,
+}
+
+
+@pytest.fixture(scope="module", params=list(CASES))
+def built(request):
+    case = CASES[request.param]()
+    return case, build(case.tris, case.meshes)
+
+
+def test_every_entry_exactly_once_with_its_scan_key(built):
+    case, b = built
+    T = case.tris.view(np.float32).reshape(-1, 16)
+    entries = scan_entries(case.tris, case.meshes)
+    placed = {}
+    for rec in list(b["prims"]) + list(b["irregular"]):
+        key, m, idx = ubits(rec[3]), ubits(rec[7]), ubits(rec[11])
+        assert (key, m, idx) not in placed
+        placed[(key, m, idx)] = rec
+        np.testing.assert_array_equal(bits(rec[[0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14]]),
+                                      bits(T[idx][[0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14]]))
+    never = [e for e in entries if e not in placed]
+    assert len(never) == b["never"]
+    for _, _, idx in never:  # only exactly-zero normals are dropped
+        assert (T[idx][12:15] == 0).all()
+    assert len(placed) + len(never) == len(entries)
+
+
+def test_tree_structure_boxes_and_cones(built):
+    case, b = built
+    N = b["nodes"]
+    if len(N) == 0:
+        return
+    Nu = N.view(np.uint32)
+    n_nodes, n_prims = len(N), len(b["prims"])
+    covered = np.zeros(n_prims, np.int32)
+
+    def verts(rec):
+        a = rec[0:3].astype(np.float64)
+        return np.stack([a, a + rec[4:7].astype(np.float64), a + rec[8:11].astype(np.float64)])
+
+    def walk(k):  # returns the index after k's subtree
+        lo, hi = N[k, 0:3], N[k, 4:7]
+        assert (lo <= hi).all()
+        assert N[k, 3] >= 0 and N[k, 7] >= 0  # margin coefficients
+        info = int(Nu[k, 14])
+        count, first = info >> 27, info & 0x07FFFFFF
+        axis, cphi, sphi = N[k, 8:11].astype(np.float64), float(N[k, 11]), float(N[k, 12])
+        assert abs(cphi * cphi + sphi * sphi - 1) < 1e-5
+        if count:
+            for p in range(first, first + count):
+                covered[p] += 1
+                v = verts(b["prims"][p])
+                assert (v >= lo - 0).all() and (v <= hi + 0).all(), (k, p)
+                n = b["prims"][p][12:15].astype(np.float64)
+                if cphi > 0:
+                    assert axis @ (n / np.linalg.norm(n)) >= cphi - 1e-6
+            end = k + 1
+        else:
+            left_end = walk(k + 1)
+            assert int(Nu[k + 1, 15]) == left_end
+            for c in (k + 1, left_end):  # children nest in the parent box
+                assert (N[c, 0:3] >= lo).all() and (N[c, 4:7] <= hi).all()
+            end = walk(left_end)
+        assert int(Nu[k, 15]) == end
+        return end
+
+    assert walk(0) == n_nodes
+    assert (covered == 1).all()
+
+
+def dir_cell(d):
+    """The kernel's dir_cell in binary32 (hrt_kernels.hip)."""
+    d = d.astype(np.float32)
+    a = np.abs(d)
+    fx = (a[:, 0] >= a[:, 1]) & (a[:, 0] >= a[:, 2])
+    fy = ~fx & (a[:, 1] >= a[:, 2])
+    face = np.where(fx, np.where(d[:, 0] < 0, 1, 0), np.where(fy, np.where(d[:, 1] < 0, 3, 2),
+                                                              np.where(d[:, 2] < 0, 5, 4)))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        u = np.where(fx, d[:, 1] / a[:, 0], np.where(fy, d[:, 2] / a[:, 1], d[:, 0] / a[:, 2])).astype(np.float32)
+        v = np.where(fx, d[:, 2] / a[:, 0], np.where(fy, d[:, 0] / a[:, 1], d[:, 1] / a[:, 2])).astype(np.float32)
+    s = np.float32(0.5 * DIR_RES)
+    iu = np.clip(((u + np.float32(1)) * s).astype(np.int64), 0, DIR_RES - 1)
+    iv = np.clip(((v + np.float32(1)) * s).astype(np.int64), 0, DIR_RES - 1)
+    return (face * DIR_RES + iu) * DIR_RES + iv
+
+
+def test_band_lists_cover_every_grazing_triangle(built):
+    case, b = built
+    prims = b["prims"]
+    if len(prims) == 0:
+        return
+    n = prims[:, 12:15].astype(np.float64)
+    nh = n / np.linalg.norm(n, axis=1, keepdims=True)
+    rng = np.random.default_rng(3)
+    d = rng.normal(size=(6000, 3))
+    # plus directions right at cube-face edges and corners, and exactly in some triangles' planes
+    edge = np.array([[1, 1, 0.3], [1, -1, 0.2], [1, 1, 1], [-1, 1, -1], [0.5, 1, 1], [1, 0, 0], [0, 0, -1]], float)
+    t = rng.integers(len(nh), size=300)
+    inplane = np.cross(nh[t], rng.normal(size=(300, 3)))
+    d = np.concatenate([d, edge, inplane])
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    cells = dir_cell(d)
+    band_idx = b["band"][:, 3]
+    off = b["band_off"]
+    lo, hi = -(float(TAU_G) + 1e-5), 2e-5
+    for i in range(len(d)):
+        dn = nh @ d[i].astype(np.float64)
+        need = np.nonzero((dn > lo) & (dn < hi))[0]
+        if len(need) == 0:
+            continue
+        c = cells[i]
+        have = set(band_idx[off[c]:off[c + 1]].tolist())
+        missing = [k for k in need if k not in have]
+        assert not missing, f"direction {d[i]} cell {c}: band prims {missing[:5]} missing"
+
+
+def test_band_entries_are_unit_normals_of_their_prims(built):
+    case, b = built
+    if len(b["band"]) == 0:
+        return
+    band = b["band"]
+    k = band[:, 3]
+    n = b["prims"][k, 12:15].astype(np.float64)
+    nh = n / np.linalg.norm(n, axis=1, keepdims=True)
+    stored = band[:, :3].view(np.float32).astype(np.float64)
+    assert np.abs(stored - nh).max() < 2e-7
+
+
+def test_not_built_above_the_mesh_limit():
+    rng = np.random.default_rng(1)
+    meshes = [E.RayTracingMesh(E.Mesh(rng.uniform(-1, 1, (3, 3)).astype(np.float32), np.arange(3, dtype=np.uint32)),
+                               E.LambertianMaterial([0.5, 0.5, 0.5])) for _ in range(65)]
+    st = E.RayTracerSettings(num_samples=1, max_bounces=1, use_environment_lighting=True, mesh_data=meshes)
+    case = SceneCase(settings=st, camera=E.Camera([0, 0, -5], [0, 0, 1]), size=(4, 4))
+    assert build(case.tris, case.meshes) is None
+
+
+@pytest.mark.parametrize("leaf", [1, 2, 16])
+def test_leaf_sizes(leaf):
+    case = SceneCase("box", (8, 8), 1, 1)
+    b = build(case.tris, case.meshes, leaf)
+    counts = (b["nodes"].view(np.uint32)[:, 14] >> 27)
+    assert counts.max() <= leaf and counts.sum() == len(b["prims"])
