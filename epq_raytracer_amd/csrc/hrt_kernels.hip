@@ -319,19 +319,23 @@ __device__ __forceinline__ void tri_exact(const TriPre& q, uint32_t i, uint32_t 
 // Two-stage test of one triangle record (a, e1, e2, n as float4 with unused w): stage 1 computes
 // ao and num_t and leaves when no lane has num_t > 0 (necessary for dist > 0.001 since inv > 0);
 // stage 2 completes the pre-test.
+// Lanes with on == false take part in the arithmetic but never in a decision (callers use it for the
+// per-lane mesh filter instead of an exec-mask branch around each triangle).
 __device__ __forceinline__ void tri_two_stage(const float4& A, const float4& B, const float4& C, const float4& N,
-                                              uint32_t i, uint32_t m, f3 o, f3 d, Closest& c, float& best_k) {
+                                              uint32_t i, uint32_t m, f3 o, f3 d, Closest& c, float& best_k,
+                                              bool on = true) {
   const f3 n = mk(N.x, N.y, N.z);
   const f3 ao = o - mk(A.x, A.y, A.z);
   TriPre q;
   q.num_t = dot(ao, n);
-  if (!__any(q.num_t > 0.0f)) return;
+  const bool front = on & (q.num_t > 0.0f);
+  if (!__any(front)) return;
   const float dn = dot(d, n);
   const f3 dao = cross(ao, d);
   q.num_u = dot(mk(C.x, C.y, C.z), dao);
   q.num_v = dot(mk(B.x, B.y, B.z), dao);
   q.det = -dn;
-  q.cand = (dn < 0.0f) & (q.num_t > 0.0f) & !pre_reject(q, best_k);
+  q.cand = (dn < 0.0f) & front & !pre_reject(q, best_k);
   if (__builtin_expect(__any(q.cand), 0)) {
     if (q.cand) tri_exact(q, i, m, c, best_k);
   }
@@ -773,7 +777,8 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
     if (sec) tests += pass ? mesh.len : 0u;
     if (!__any(pass)) continue;
     const uint32_t k0 = mesh.first_index, k1 = k0 + mesh.len;
-    for (uint32_t base = k0; base < k1; base += 64) {
+    for (uint32_t base_v = k0; base_v < k1; base_v += 64) {
+      const uint32_t base = __builtin_amdgcn_readfirstlane(base_v);  // uniform: scalar survivor indices
       const uint32_t k = base + lane;
       bool keep = false;
       if (k < k1) {
@@ -806,7 +811,7 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
           dg.sec_stage2 += __any(s2) ? 1u : 0u;
           dg.sec_front += __any(s2 && dot(d, mk(N.x, N.y, N.z)) < 0.0f) ? 1u : 0u;
         }
-        if (pass) tri_two_stage(A, B, C, N, kk, (uint32_t)m, o, d, c, best_k);
+        tri_two_stage(A, B, C, N, kk, (uint32_t)m, o, d, c, best_k, pass);
       }
     }
   }
