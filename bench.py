@@ -146,27 +146,32 @@ def main():
         traffic = None
         pmc_note = None
         executed_flops = None
+        basis = "unmeasured (no rocprofv3 PMC record for this kernel and scene)"
         if os.path.exists(args.pmc_json):
             with open(args.pmc_json) as f:
                 pmc = json.load(f)
             wl = pmc.get("workload", {})
-            if (wl.get("scene"), wl.get("width"), wl.get("height"), wl.get("spp"), wl.get("bounces"),
-                    wl.get("variant"), pmc.get("kernel")) == (args.scene, W, H, args.spp, args.bounces, args.variant,
-                                                              kernel_sym):
-                per_test = pmc.get("executed_flops_per_reference_test")
-                if world == 1:
-                    traffic = pmc.get("hbm_bytes_per_trace_launch")
-                    executed_flops = pmc.get("executed_fp32_flops_per_trace_launch")
-                elif per_test:  # a rank's launch covers a row-tile subset: scale by its own work
-                    executed_flops = per_test * tests_per_launch
-                    if pmc.get("hbm_bytes_per_trace_launch"):
-                        traffic = pmc["hbm_bytes_per_trace_launch"] * ctx.local_rows / H
+            same_kernel = (wl.get("scene"), pmc.get("kernel")) == (args.scene, kernel_sym)
+            exact = same_kernel and (wl.get("width"), wl.get("height"), wl.get("spp"), wl.get("bounces"),
+                                     wl.get("variant")) == (W, H, args.spp, args.bounces, args.variant)
+            per_test = pmc.get("executed_flops_per_reference_test")
+            if exact and world == 1:
+                traffic = pmc.get("hbm_bytes_per_trace_launch")
+                executed_flops = pmc.get("executed_fp32_flops_per_trace_launch")
+                basis = "executed (rocprofv3 PMC FLOP count per launch / live launch time)"
+            elif same_kernel and per_test:
+                # this rank's launch: the profiled kernel's FLOPs per reference triangle test x its own tests
+                executed_flops = per_test * tests_per_launch
+                if exact and pmc.get("hbm_bytes_per_trace_launch"):
+                    traffic = pmc["hbm_bytes_per_trace_launch"] * ctx.local_rows / H
+                basis = ("executed (rocprofv3 PMC FLOPs per reference test of this kernel on " +
+                         f"{wl.get('scene')} {wl.get('width')}x{wl.get('height')} {wl.get('spp')}spp, x this launch's tests)")
+            if executed_flops:
                 pmc_note = os.path.relpath(args.pmc_json, ROOT)
-        # achieved = FP32 FLOPs the kernel executes per launch (hardware-counted by rocprofv3 on this
-        # deterministic workload: 64 * (2*FMA + MUL + ADD) wave-instructions; N > 1: the same
-        # FLOPs-per-reference-test ratio applied to this rank's launches) / the live launch time.
-        # Without a matching PMC record the reference-equivalent rate is reported (see achieved_basis).
-        achieved_tf = executed_flops / (kern_ms * 1e-3) / 1e12 if executed_flops else algorithmic_tf
+        # achieved = FP32 FLOPs the kernel executes per launch (hardware-counted by rocprofv3:
+        # 64 * (2*FMA + MUL + ADD) wave-instructions) / the live launch time.  The reference-equivalent
+        # rate (algorithmic_tflops) can exceed the hardware peak and is never reported as achieved.
+        achieved_tf = executed_flops / (kern_ms * 1e-3) / 1e12 if executed_flops else None
         line = {
             "metric": "Mrays/s (island.obj 1080p 64spp 8-bounce path-trace segments per second)",
             "value": round(value, 3),
@@ -190,11 +195,11 @@ def main():
             "segments_per_step": segs_all // args.steps,
             "tri_tests_per_step": tests_all // args.steps,
             "paths_per_s": W * H * args.spp / (elapsed / args.steps),
-            "roofline": {"bound": "valu-fp32", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
-                         "traffic": traffic,
-                         "achieved_basis": "executed (rocprofv3 PMC FLOP count per launch / live launch time)"
-                                           if executed_flops else "reference-equivalent (38 FLOP x reference tests)",
+            "roofline": {"bound": "valu-fp32",
+                         "achieved": round(achieved_tf, 3) if achieved_tf is not None else None,
+                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4) if achieved_tf is not None else None,
+                         "traffic": traffic, "achieved_basis": basis,
                          "algorithmic_tflops": round(algorithmic_tf, 3),
                          "kernel": kernel_sym,
                          "kernel_ms": round(kern_ms, 3), "flop_per_test": FLOP_PER_TEST,
