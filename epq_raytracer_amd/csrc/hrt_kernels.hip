@@ -575,11 +575,15 @@ __device__ __forceinline__ void primary_exact(const kfloat* ct, uint32_t k, floa
 // convex), widened by 1e-5 in cosine for rounding.  The bundle cull against that cap runs ONCE per
 // wave; its survivors (camera-list index | mesh << 27, in buffer order) are the only triangles any
 // primary segment of the wave can hit, so each primary iteration tests just those.  The list lives
-// in one VGPR (entry i in lane i, read back with v_readlane): no LDS traffic on the primary path.
-constexpr uint32_t kTileCap = 64;  // list entries per wave; more -> per-iteration cull
+// in one VGPR (entry i in lane i, read back with v_readlane; up to 64 entries) in the LDS-resident
+// kernels, and in a per-wave LDS slice of kTileCapLds entries in the others (dense scenes put
+// hundreds of triangles in a tile's cap).  A wave whose list overflows culls per iteration.
+constexpr uint32_t kTileCapVgpr = 64;
+constexpr uint32_t kTileCapLds = 1024;
 
 struct TileList {
-  uint32_t v;  // lane i: entry i
+  uint32_t v;      // VGPR list: lane i holds entry i
+  uint32_t* lds;   // LDS list (nullptr: VGPR list)
   uint32_t n;
   bool ok;
 };
@@ -619,9 +623,10 @@ __device__ __forceinline__ bool bundle_keep(const float4* __restrict__ cr, uint3
 }
 
 // Builds the wave's list (all 64 lanes active; the caller synchronises before reading it).
-__device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool active, f3 centre) {
+__device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool active, f3 centre, uint32_t* lds) {
   const hrt_push_constants& pc = P.pc;
-  TileList t{0u, 0u, false};
+  TileList t{0u, lds, 0u, false};
+  const uint32_t cap = lds ? kTileCapLds : kTileCapVgpr;
   if (pc.num_meshes > 32 || !__any(active)) return t;
   bool ok;
   const Bundle b = tile_bundle(pc, active, centre, ok);
@@ -633,16 +638,25 @@ __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool a
       const uint32_t k = base + lane;
       const bool keep = k < k1 && bundle_keep(P.cam_cull, k, b);
       unsigned long long mask = __ballot(keep);
-      if (t.n + (uint32_t)__popcll(mask) > kTileCap) return t;  // ok stays false: per-iteration cull
-      while (mask) {  // few survivors: append each to the next lane
-        const uint32_t e = (base + (uint32_t)__builtin_ctzll(mask)) | ((uint32_t)m << 27);
-        mask &= mask - 1ull;
-        t.v = lane == t.n ? e : t.v;
-        ++t.n;
+      const uint32_t cnt = (uint32_t)__popcll(mask);
+      if (t.n + cnt > cap) return t;  // ok stays false: per-iteration cull
+      if (lds) {  // lane-parallel append in buffer order
+        if (keep) lds[t.n + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = k | ((uint32_t)m << 27);
+        t.n += cnt;
+      } else {
+        while (mask) {  // few survivors: append each to the next lane
+          const uint32_t e = (base + (uint32_t)__builtin_ctzll(mask)) | ((uint32_t)m << 27);
+          mask &= mask - 1ull;
+          t.v = lane == t.n ? e : t.v;
+          ++t.n;
+        }
       }
     }
   }
   t.ok = true;
+  // the wave reads its own LDS writes back; a wave's LDS accesses complete in order, so only the
+  // compiler needs fencing
+  __builtin_amdgcn_wave_barrier();
   return t;
 }
 
@@ -664,7 +678,8 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
   float best_k = c.t * kOnePlus;
   const kfloat* ct = to_const(P.cam_tris);
   for (uint32_t i = 0; i < tl.n; ++i) {
-    const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
+    const uint32_t e = tl.lds ? __builtin_amdgcn_readfirstlane(tl.lds[i])
+                              : (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
     const bool pass = (pass_mask >> m) & 1u;
     if (!__any(pass)) continue;
@@ -1058,7 +1073,7 @@ enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2 };
 
 template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, const CullSrc& csrc,
-                                                  const BvhSrc& bsrc = BvhSrc{}) {
+                                                  const BvhSrc& bsrc = BvhSrc{}, uint32_t* list_lds = nullptr) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
   const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
@@ -1074,7 +1089,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     centre = mk(rc.x, rc.y, rc.z);
   }
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
-  const TileList tl = build_tile_list(P, active, centre);
+  const TileList tl = build_tile_list(P, active, centre, list_lds);
   int sample = 0;
   Path p;
   p.bounce = pc.max_bounces + 1;
@@ -1172,10 +1187,12 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
 
 template <bool D>
 __global__ __launch_bounds__(256) void trace_bundle(TraceParams P) {
+  __shared__ uint32_t lists[4 * kTileCapLds];
   uint32_t x, lr;
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  trace_fused_split<kBounceBrute, D>(P, x, lr, CullGlobal{T, to_const(T)});
+  trace_fused_split<kBounceBrute, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhGlobal{},
+                                     lists + (threadIdx.x >> 6) * kTileCapLds);
 }
 
 #ifndef HRT_CULL_WAVES
@@ -1184,18 +1201,22 @@ __global__ __launch_bounds__(256) void trace_bundle(TraceParams P) {
 template <bool D>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HRT_CULL_WAVES))) void trace_bundle_cull(
     TraceParams P) {
+  __shared__ uint32_t lists[4 * kTileCapLds];
   uint32_t x, lr;
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  trace_fused_split<kBounceCull, D>(P, x, lr, CullGlobal{T, to_const(T)});
+  trace_fused_split<kBounceCull, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhGlobal{},
+                                    lists + (threadIdx.x >> 6) * kTileCapLds);
 }
 
 template <bool D>
 __global__ __launch_bounds__(256) void trace_bundle_bvh(TraceParams P) {
+  __shared__ uint32_t lists[4 * kTileCapLds];
   uint32_t x, lr;
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhGlobal{P.bvh_nodes, P.bvh_prims});
+  trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhGlobal{P.bvh_nodes, P.bvh_prims},
+                                   lists + (threadIdx.x >> 6) * kTileCapLds);
 }
 
 
