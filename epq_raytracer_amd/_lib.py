@@ -99,6 +99,7 @@ EXPORTED_SYMBOLS = (
     "hrt_abi_version", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate",
     "hrt_read_image", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
     "hrt_get_diagnostics", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
+    "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory",
     "hrt_stream", "hrt_last_error",
     "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
     "hrt_debug_bvh_build",
@@ -144,6 +145,11 @@ def load() -> ctypes.CDLL:
         "hrt_get_scene_info": (c_int32, [P, P, c_uint32]),
         "hrt_generate_rays": (c_int32, [P, c_float, c_float, POINTER(c_float), POINTER(c_float)]),
         "hrt_read_rays": (c_int32, [P, P, c_uint32]),
+        "hrt_import_external_memory": (c_int32, [P, c_int32, c_uint64, c_uint64, c_uint64, POINTER(c_void_p)]),
+        "hrt_release_external_memory": (c_int32, [P, P]),
+        "hrt_debug_export_memory": (c_int32, [c_int32, c_uint64, POINTER(c_int32), POINTER(c_void_p),
+                                              POINTER(c_uint64)]),
+        "hrt_debug_unmap_memory": (c_int32, [P, c_uint64]),
         "hrt_debug_bvh_build": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, P, c_uint64, P, c_uint64, P,
                                           c_uint64, P, c_uint64, P, c_uint64]),
         "hrt_host_ray_grid": (c_uint32, [c_uint32, c_uint32, c_float, c_float, POINTER(c_float), POINTER(c_float),

@@ -80,6 +80,11 @@ struct hrt_context {
   uint32_t sec_batch = 48;
   int last_kernel = 0, last_block = 0;  // what the last hrt_trace launched (hrt_stats)
 
+  struct Import {
+    hipExternalMemory_t mem;
+    void* ptr;
+  };
+  std::vector<Import> imports;           // hrt_import_external_memory (released by hrt_destroy)
   std::vector<EventPair> event_pool;     // reusable
   std::vector<EventPair> pending;        // recorded, not yet harvested
   uint64_t traces = 0, accumulates = 0;
@@ -237,6 +242,15 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
   free_dev(ctx->cam_meta);
   free_dev(ctx->cam_tris);
   free_dev(ctx->cam_cull);
+  free_dev(ctx->bvh_nodes);
+  free_dev(ctx->bvh_prims);
+  free_dev(ctx->bvh_irregular);
+  free_dev(ctx->bvh_band_off);
+  free_dev(ctx->bvh_band);
+  free_dev(ctx->bvh_entries);
+  free_dev(ctx->bvh_keybase);
+  free_dev(ctx->tile_counter);
+  for (auto& im : ctx->imports) (void)hipDestroyExternalMemory(im.mem);
   for (auto& ev : ctx->event_pool) {
     (void)hipEventDestroy(ev.start);
     (void)hipEventDestroy(ev.stop);
@@ -524,6 +538,85 @@ extern "C" hrt_status hrt_generate_rays(hrt_context* ctx, float camera_focal_len
   if (n) HRT_HIP(ctx, hrt::launch_make_rays(ctx->rays, ctx->width, ctx->height, first, px, py, ctx->stream));
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->n_rays = (uint32_t)want;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_import_external_memory(hrt_context* ctx, int fd, uint64_t size, uint64_t offset,
+                                                 uint64_t bytes, void** dev_ptr) {
+  if (!ctx || fd < 0 || !dev_ptr || bytes == 0 || offset + bytes > size)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_import_external_memory: bad fd / size / range");
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  hipExternalMemoryHandleDesc desc{};
+  desc.type = hipExternalMemoryHandleTypeOpaqueFd;
+  desc.handle.fd = fd;
+  desc.size = size;
+  hipExternalMemory_t mem = nullptr;
+  HRT_HIP(ctx, hipImportExternalMemory(&mem, &desc));
+  hipExternalMemoryBufferDesc bd{};
+  bd.offset = offset;
+  bd.size = bytes;
+  void* ptr = nullptr;
+  if (hipError_t e = hipExternalMemoryGetMappedBuffer(&ptr, mem, &bd); e != hipSuccess) {
+    (void)hipDestroyExternalMemory(mem);
+    return hip_fail(ctx, e, "hipExternalMemoryGetMappedBuffer");
+  }
+  ctx->imports.push_back({mem, ptr});
+  *dev_ptr = ptr;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_release_external_memory(hrt_context* ctx, void* dev_ptr) {
+  if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
+  for (size_t i = 0; i < ctx->imports.size(); ++i) {
+    if (ctx->imports[i].ptr == dev_ptr) {
+      hrt_status st = hrt_synchronize(ctx);  // no pending write into it
+      if (st != HRT_OK) return st;
+      HRT_HIP(ctx, hipDestroyExternalMemory(ctx->imports[i].mem));
+      ctx->imports.erase(ctx->imports.begin() + (long)i);
+      return HRT_OK;
+    }
+  }
+  return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_release_external_memory: not an imported pointer");
+}
+
+// Test support: device memory exported as a POSIX fd (HIP virtual memory management), i.e. what the
+// presenting API hands to hrt_import_external_memory; *ptr is the exporter's own mapping of it.
+extern "C" hrt_status hrt_debug_export_memory(int device, uint64_t bytes, int* fd, void** ptr, uint64_t* size) {
+  if (!fd || !ptr || !size || bytes == 0) return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "bad arguments");
+  hipError_t e = hipSetDevice(device);
+  hipMemAllocationProp prop{};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  prop.requestedHandleTypes = hipMemHandleTypePosixFileDescriptor;
+  size_t gran = 0;
+  if (e == hipSuccess) e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum);
+  const size_t sz = gran ? (bytes + gran - 1) / gran * gran : bytes;
+  hipMemGenericAllocationHandle_t h{};
+  if (e == hipSuccess) e = hipMemCreate(&h, sz, &prop, 0);
+  if (e == hipSuccess) e = hipMemExportToShareableHandle(fd, h, hipMemHandleTypePosixFileDescriptor, 0);
+  void* va = nullptr;
+  if (e == hipSuccess) e = hipMemAddressReserve(&va, sz, 0, nullptr, 0);
+  if (e == hipSuccess) e = hipMemMap(va, sz, 0, h, 0);
+  if (e == hipSuccess) {
+    hipMemAccessDesc acc{};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    e = hipMemSetAccess(va, sz, &acc, 1);
+  }
+  if (e == hipSuccess) e = hipMemRelease(h);  // the mapping keeps the allocation alive
+  if (e != hipSuccess) {
+    g_create_error = std::string("export: ") + hipGetErrorString(e);
+    return HRT_ERR_HIP;
+  }
+  *ptr = va;
+  *size = sz;
+  return HRT_OK;
+}
+
+extern "C" hrt_status hrt_debug_unmap_memory(void* ptr, uint64_t size) {
+  if (hipMemUnmap(ptr, size) != hipSuccess || hipMemAddressFree(ptr, size) != hipSuccess) return HRT_ERR_HIP;
   return HRT_OK;
 }
 

@@ -140,6 +140,17 @@ class HrtContext:
                     "hrt_generate_rays")
         return jit.value
 
+    def import_external(self, fd: int, size: int, offset: int, nbytes: int) -> int:
+        """hrt_import_external_memory: device pointer (int) to [offset, offset + nbytes) of the fd."""
+        ptr = ctypes.c_void_p()
+        self._check(self.lib.hrt_import_external_memory(self.handle, int(fd), int(size), int(offset), int(nbytes),
+                                                        ctypes.byref(ptr)), "hrt_import_external_memory")
+        return int(ptr.value)
+
+    def release_external(self, dev_ptr: int):
+        self._check(self.lib.hrt_release_external_memory(self.handle, ctypes.c_void_p(dev_ptr)),
+                    "hrt_release_external_memory")
+
     def read_rays(self) -> np.ndarray:
         out = np.empty(self.width * self.height, dtype=_lib.RAY_DTYPE)
         self._check(self.lib.hrt_read_rays(self.handle, _lib.ptr(out), len(out)), "hrt_read_rays")

@@ -257,6 +257,20 @@ hrt_status hrt_generate_rays(hrt_context* ctx, float camera_focal_length, float 
                              float* default_jitter);
 /* Copies n (<= width*height) ray records of the context to host memory (verification). */
 hrt_status hrt_read_rays(hrt_context* ctx, hrt_ray* out, uint32_t n);
+
+/* Present interop (replaces the reference's image -> texture hand-off,
+ * src/raytracing_app.rs:196-227): import memory the presenting API exported as an opaque POSIX fd
+ * (Vulkan: VK_KHR_external_memory_fd, vkGetMemoryFdKHR on the staging buffer's memory, size = its
+ * allocation size) and map [offset, offset + bytes) into *dev_ptr.  On success the fd belongs to
+ * the import.  hrt_read_image(ctx, HRT_IMG_ACCUM, fmt, *dev_ptr, bytes) then writes each frame
+ * there device to device.  Imports are released by hrt_release_external_memory or hrt_destroy. */
+hrt_status hrt_import_external_memory(hrt_context* ctx, int fd, uint64_t size, uint64_t offset, uint64_t bytes,
+                                      void** dev_ptr);
+hrt_status hrt_release_external_memory(hrt_context* ctx, void* dev_ptr);
+/* Test support for the above: device memory exported as an fd (HIP VMM) and the exporter's own
+ * mapping of it (*ptr, *size rounded to the allocation granularity); hrt_debug_unmap_memory frees it. */
+hrt_status hrt_debug_export_memory(int device, uint64_t bytes, int* fd, void** ptr, uint64_t* size);
+hrt_status hrt_debug_unmap_memory(void* ptr, uint64_t size);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
 /* HIP stream the context's work is ordered on (hipStream_t), for callers that interoperate. */

@@ -338,6 +338,37 @@ def test_trace_with_device_rays():
     assert (st.segments, st.tri_tests) == (seg, tt)
 
 
+def test_present_interop_external_memory():
+    """a frame written straight into memory the presenting API exported as an
+    fd (here exported by HIP's VMM API, as vkGetMemoryFdKHR would) equals the host read-back."""
+    import ctypes
+    lib = _lib.load()
+    case = SceneCase("box", (64, 48), 2, 4)
+    ctx = case.context()
+    ctx.trace(case.push())
+    ctx.accumulate(1)
+    nbytes = 64 * 48 * 4
+    fd, ptr, size = ctypes.c_int32(-1), ctypes.c_void_p(), ctypes.c_uint64()
+    st = lib.hrt_debug_export_memory(0, nbytes, ctypes.byref(fd), ctypes.byref(ptr), ctypes.byref(size))
+    if st != 0:
+        ctx.close()
+        pytest.skip("device memory export unsupported here: " + lib.hrt_last_error(None).decode())
+    dev = ctx.import_external(fd.value, size.value, 0, nbytes)
+    ctx.read_into(_lib.IMG_ACCUM, _lib.FMT_RGBA8, dev, nbytes)  # device destination
+    ctx.synchronize()
+    hip = ctypes.CDLL("libamdhip64.so")
+    got = np.empty((48, 64, 4), np.uint8)
+    assert hip.hipMemcpy(ctypes.c_void_p(got.ctypes.data), ptr, ctypes.c_size_t(nbytes), 2) == 0  # D2H
+    ref = ctx.read(_lib.IMG_ACCUM)
+    ctx.release_external(dev)
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        ctx.release_external(dev)
+    ctx.close()
+    assert lib.hrt_debug_unmap_memory(ptr, size.value) == 0
+    np.testing.assert_array_equal(got, ref)
+    assert ref[..., :3].any()
+
+
 def test_errors_fail_loudly():
     case = SceneCase("box", (32, 32), 1, 1)
     ctx = E.HrtContext((32, 32), device=0)
