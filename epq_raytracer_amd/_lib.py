@@ -72,6 +72,7 @@ MODE_RGBA8, MODE_RGBA32F = 0, 1
 IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
+OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP = 5, 6, 7, 8, 9
 # hrt_kernel (include/hip_raytrace.h)
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
 KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS, KERNEL_BUNDLE_BVH_LDS = 6, 7, 8
@@ -98,7 +99,7 @@ SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh
 EXPORTED_SYMBOLS = (
     "hrt_abi_version", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate",
     "hrt_read_image", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
-    "hrt_get_diagnostics", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
+    "hrt_get_diagnostics", "hrt_get_tile_profile", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
     "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory",
     "hrt_stream", "hrt_last_error",
     "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
@@ -143,6 +144,7 @@ def load() -> ctypes.CDLL:
         "hrt_reset_stats": (c_int32, [P]),
         "hrt_get_diagnostics": (c_int32, [P, P, c_uint32]),
         "hrt_get_scene_info": (c_int32, [P, P, c_uint32]),
+        "hrt_get_tile_profile": (c_int32, [P, P, c_uint32]),
         "hrt_generate_rays": (c_int32, [P, c_float, c_float, POINTER(c_float), POINTER(c_float)]),
         "hrt_read_rays": (c_int32, [P, P, c_uint32]),
         "hrt_import_external_memory": (c_int32, [P, c_int32, c_uint64, c_uint64, c_uint64, POINTER(c_void_p)]),

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -57,7 +58,15 @@ struct hrt_context {
   float4* accum32 = nullptr;
   void* scratch = nullptr;  // format conversion for hrt_read_image
   unsigned long long* counters = nullptr;
-  uint32_t* tile_counter = nullptr;  // persistent LDS kernels' work counter
+  unsigned long long* tile_cycles = nullptr;  // diagnostics: shader clocks per 8x8 tile of the last trace
+  uint32_t* sched = nullptr;      // persistent kernels' scheduler words (hrt_kernels.h)
+  uint32_t* tile_cost = nullptr;  // per 8x8 tile
+  uint32_t* item_buf = nullptr;   // planned work items (tiles x 8)
+  bool plan_valid = false;        // tile_cost describes the last trace (same size, persistent kernel)
+  uint32_t split_k = 1, split_prio = 1;
+  int32_t split_factor = -1;  // auto
+  uint32_t grid_cus = 0;  // HRT_OPT_GRID_CUS (0: every CU)
+  uint32_t coop = 1;      // HRT_OPT_COOP
   uint32_t num_cus = 0;
   uint32_t* cam_meta = nullptr;   // bundle variants: cam_start[n_meshes], cam_count[n_meshes]
   uint32_t cam_capacity = 0;      // sum of mesh lengths
@@ -93,6 +102,7 @@ struct hrt_context {
   std::string err;
 
   size_t npix() const { return (size_t)local_rows * width; }
+  size_t num_tiles() const { return (size_t)((width + 7) / 8) * ((local_rows + 7) / 8); }
 };
 
 namespace {
@@ -206,7 +216,14 @@ extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_
   if ((e = hipMalloc(&ctx->scratch, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(scratch)"));
   if ((e = hipMalloc((void**)&ctx->counters, kNumCounters * sizeof(unsigned long long))) != hipSuccess)
     return bail(hip_fail(ctx, e, "hipMalloc(counters)"));
-  if ((e = hipMalloc((void**)&ctx->tile_counter, 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(tiles)"));
+  {
+    const size_t tiles = ctx->num_tiles();
+    if ((e = hipMalloc((void**)&ctx->sched, 256 * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(sched)"));
+    if ((e = hipMalloc((void**)&ctx->tile_cost, (tiles ? tiles : 1) * 4)) != hipSuccess)
+      return bail(hip_fail(ctx, e, "hipMalloc(tile costs)"));
+    if ((e = hipMalloc((void**)&ctx->item_buf, (tiles ? tiles : 1) * 8 * 4)) != hipSuccess)
+      return bail(hip_fail(ctx, e, "hipMalloc(items)"));
+  }
   {
     int cus = 0;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device)) != hipSuccess)
@@ -239,6 +256,7 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
   free_dev(ctx->accum32);
   free_dev(ctx->scratch);
   free_dev(ctx->counters);
+  free_dev(ctx->tile_cycles);
   free_dev(ctx->cam_meta);
   free_dev(ctx->cam_tris);
   free_dev(ctx->cam_cull);
@@ -249,7 +267,9 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
   free_dev(ctx->bvh_band);
   free_dev(ctx->bvh_entries);
   free_dev(ctx->bvh_keybase);
-  free_dev(ctx->tile_counter);
+  free_dev(ctx->sched);
+  free_dev(ctx->tile_cost);
+  free_dev(ctx->item_buf);
   for (auto& im : ctx->imports) (void)hipDestroyExternalMemory(im.mem);
   for (auto& ev : ctx->event_pool) {
     (void)hipEventDestroy(ev.start);
@@ -347,6 +367,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   ctx->bvh_info[5] = (uint32_t)(bvh.band_list.size() / 4);
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
   if (!keep_rays) ctx->n_rays = n_rays;
+  ctx->plan_valid = false;  // tile costs describe the old scene
   ctx->n_spheres = n_spheres;
   ctx->n_tris = n_tris;
   ctx->n_meshes = n_meshes;
@@ -378,6 +399,11 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.img32 = ctx->trace32;
   p.counters = ctx->counters_on ? ctx->counters : nullptr;
   p.diag = ctx->diag_on ? ctx->counters + 3 : nullptr;
+  if (ctx->diag_on && !ctx->tile_cycles)
+    HRT_HIP(ctx, hipMalloc((void**)&ctx->tile_cycles, ctx->num_tiles() * 4 * sizeof(unsigned long long)));
+  p.tile_cycles = ctx->diag_on ? ctx->tile_cycles : nullptr;
+  if (ctx->diag_on)
+    HRT_HIP(ctx, hipMemsetAsync(ctx->tile_cycles, 0, ctx->num_tiles() * 4 * sizeof(unsigned long long), ctx->stream));
   p.pc = *pc;
   p.local_rows = ctx->local_rows;
   p.row_tile = ctx->row_tile;
@@ -390,8 +416,15 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.cam_tris = ctx->cam_tris;
   p.cam_cull = ctx->cam_cull;
   p.sec_batch = ctx->sec_batch;
-  p.tile_counter = ctx->tile_counter;
-  p.num_cus = ctx->num_cus;
+  p.sched = ctx->sched;
+  p.tile_cost = ctx->tile_cost;
+  p.item_buf = ctx->item_buf;
+  p.split_k = ctx->split_k;
+  p.split_factor = ctx->split_factor;
+  p.split_prio = ctx->split_prio;
+  p.coop = ctx->coop;
+  p.plan_valid = ctx->plan_valid ? 1u : 0u;
+  p.num_cus = ctx->grid_cus ? std::min(ctx->grid_cus, ctx->num_cus) : ctx->num_cus;
   p.bvh_nodes = ctx->bvh_info[4] ? ctx->bvh_nodes : nullptr;
   p.bvh_prims = ctx->bvh_prims;
   p.bvh_irregular = ctx->bvh_irregular;
@@ -417,6 +450,9 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   }
   HRT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
   hipError_t e = hrt::launch_trace(p, variant, ctx->stream, &ctx->last_kernel, &ctx->last_block);
+  // the persistent kernels recorded this trace's tile costs: the next one can follow a plan
+  ctx->plan_valid = e == hipSuccess && (ctx->last_kernel == HRT_KERNEL_BUNDLE_CULL_LDS ||
+                                        ctx->last_kernel == HRT_KERNEL_BUNDLE_BVH_LDS);
   if (e != hipSuccess) {
     ctx->event_pool.push_back(ev);
     return hip_fail(ctx, e, "trace kernel launch");
@@ -629,6 +665,15 @@ extern "C" hrt_status hrt_read_rays(hrt_context* ctx, hrt_ray* out, uint32_t n) 
   return HRT_OK;
 }
 
+extern "C" hrt_status hrt_get_tile_profile(hrt_context* ctx, uint64_t* out, uint32_t count) {
+  if (!ctx || !out || count > 4 * ctx->num_tiles() || !ctx->tile_cycles)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_get_tile_profile: needs HRT_OPT_COUNTERS = 2 and a trace");
+  hrt_status st = hrt_synchronize(ctx);
+  if (st != HRT_OK) return st;
+  HRT_HIP(ctx, hipMemcpy(out, ctx->tile_cycles, (size_t)count * 8, hipMemcpyDeviceToHost));
+  return HRT_OK;
+}
+
 extern "C" hrt_status hrt_get_scene_info(hrt_context* ctx, uint32_t* out, uint32_t count) {
   if (!ctx || !out || count > HRT_NUM_SCENE_INFO) return HRT_ERR_INVALID_ARGUMENT;
   for (uint32_t i = 0; i < count; ++i) out[i] = ctx->bvh_info[i];
@@ -663,6 +708,28 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
     case HRT_OPT_SECONDARY_BATCH:
       if (value < 1 || value > 64) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "secondary batch must be in [1, 64]");
       ctx->sec_batch = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_SPLIT:
+      if (value != 1 && value != 2 && value != 4 && value != 8)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "split must be 1, 2, 4 or 8");
+      ctx->split_k = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_SPLIT_FACTOR:
+      if (value < -1 || value > 1000000)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "split factor must be -1 (auto) or 0..1000000");
+      ctx->split_factor = (int32_t)value;
+      return HRT_OK;
+    case HRT_OPT_PRIORITY:
+      if (value < 0 || value > 2) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "priority must be 0, 1 or 2");
+      ctx->split_prio = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_COOP:
+      if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "coop must be 0 or 1");
+      ctx->coop = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_GRID_CUS:
+      if (value < 0) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "grid CUs must be >= 0");
+      ctx->grid_cus = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_BVH_LEAF_SIZE:
       if (value < 1 || value > hrt::kBvhMaxLeafCount)

@@ -18,6 +18,8 @@ struct TraceParams {
   float4* img32;                 // local_rows x W float4 (RGBA32F mode) or nullptr
   unsigned long long* counters;  // [0] segments, [1] triangle tests, [2] wave steps; nullptr = off
   unsigned long long* diag;      // HRT_OPT_COUNTERS = 2: cull diagnostics (HRT_DIAG_*), else nullptr
+  unsigned long long* tile_cycles;  // HRT_OPT_COUNTERS = 2: per 8x8 tile {clocks, bounce iterations,
+                                    // bounce survivors, bounce clocks}, else nullptr
   hrt_push_constants pc;
   uint32_t local_rows, row_tile, part_index, part_count;
   uint32_t n_tris;               // uploaded triangle count (LDS staging)
@@ -28,7 +30,19 @@ struct TraceParams {
   float4* cam_tris;              // 4 float4 per record: (ao, num_t) (e1, index bits) (e2, -) (n, -)
   float4* cam_cull;              // 5 float4 per record: bundle-cull linear forms + margins
   uint32_t sec_batch;            // bounce segments run once this many lanes of a wave wait (1..64)
-  uint32_t* tile_counter;        // LDS variants (persistent): next 8x8 tile, reset by launch_trace
+  // Persistent (LDS) variants' scheduler: sched[0] work counter, [1] item count, [2] heavy tiles,
+  // [3] first heavy cost bucket, [5] cooperative-item counter, [6..7] u64 sum of tile costs,
+  // [8..199] planner histogram / offsets / cursors (256 words); tile_cost per 8x8 tile (shader clocks / 16, this trace);
+  // item_buf (tiles x 8) the planned items; items = item_buf when this trace follows a plan.
+  uint32_t* sched;
+  uint32_t* tile_cost;
+  uint32_t* item_buf;
+  const uint32_t* items;
+  uint32_t split_k;              // items per heavy tile (1 = no splitting; 2, 4, 8)
+  int32_t split_factor;          // heavy: cost > split_factor x a resident wave's share (-1: auto)
+  uint32_t split_prio;           // heavy items run at raised wave priority (s_setprio 3)
+  uint32_t coop;                 // heavy tiles run cooperatively by a whole workgroup (BUNDLE_CULL_LDS)
+  uint32_t plan_valid;           // tile_cost holds the previous trace's costs of this context
   uint32_t num_cus;              // compute units of the device (persistent grid size)
   // BUNDLE_BVH: bounce-segment hierarchy built by hrt_set_scene (hrt_bvh.h records); nullptr = none.
   const float4* bvh_nodes;       // 4 float4 per node, preorder with escape indices

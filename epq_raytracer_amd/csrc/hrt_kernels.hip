@@ -763,6 +763,39 @@ struct CullLds {  // LDS image, 3 float4 per triangle: (a, n.x) (n.yz, e1.xy) (e
   }
 };
 
+// ---- cooperative tiles ------------------------------------------------------------------------------
+// A heavy tile's frame time is its sequential chain of bounce batches, each a dependent survivor loop
+// (profiles/r01k_*).  In a cooperative tile every wave of the workgroup runs the same 64 pixels with
+// identical state; the bounce cull's 64-triangle chunks (numbered across meshes in scan order) are
+// dealt out over the W waves, chunk j to wave j mod W, and the per-lane closest hits are merged with
+// one 64-bit LDS min per lane over
+// key = bits(t) << 32 | id, id = 0 for "no triangle" (the sphere / miss result every wave shares)
+// and 1 + (mesh << 26 | index) for a triangle.  For t >= 0 the float bits order like t, and the
+// reference's scan (spheres, then meshes in order, triangles in index order, strict <) keeps the
+// first of equal distances, which is the lowest id: the merge gives exactly the serial result.
+// Slots are triple-buffered so that one barrier per batch suffices: wave 0 clears slot r+1 before
+// the barrier of batch r, when every wave has finished reading it (batch r-2).
+struct Coop {
+  uint32_t w, W;                 // this wave, waves in the group (1: not cooperative)
+  unsigned long long* ex;        // 3 x 64 slots (LDS)
+  uint32_t round;
+  uint32_t work;                 // this wave's share of the tile's work units (the planner's cost)
+};
+
+__device__ __forceinline__ void coop_merge(Coop& co, Closest& c) {
+  const uint32_t lane = threadIdx.x & 63;
+  unsigned long long* slot = co.ex + 64 * (co.round % 3);
+  if (co.w == 0) co.ex[64 * ((co.round + 1) % 3) + lane] = ~0ull;
+  const uint32_t id = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
+  const unsigned long long key = ((unsigned long long)__float_as_uint(c.t) << 32) | id;
+  atomicMin(&slot[lane], key);
+  __syncthreads();
+  const unsigned long long best = slot[lane];
+  ++co.round;
+  const uint32_t bid = (uint32_t)best;
+  if (bid != 0) c = Closest{__uint_as_float((uint32_t)(best >> 32)), 2, (bid - 1u) & 0x03FFFFFFu, (bid - 1u) >> 26};
+}
+
 // Bounce segments with a lane-parallel pre-cull (BUNDLE_CULL).  For the bounce lanes (origins o_l,
 // directions d_l) and triangle (a, n):
 //   S1  num_t = (o - a).n is linear in o: if max over the lanes' origin box B of (o - a).n
@@ -773,7 +806,7 @@ struct CullLds {  // LDS image, 3 float4 per triangle: (a, n.x) (n.yz, e1.xy) (e
 // Called with ALL 64 lanes active.
 template <bool D, class Src>
 __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const TraceParams& P, const Src& src, bool sec,
-                                                      f3 o, f3 d, uint32_t& tests, Closest& c, Diag& dg) {
+                                                      f3 o, f3 d, uint32_t& tests, Closest& c, Diag& dg, Coop& co) {
   const hrt_push_constants& pc = P.pc;
   const float inf = __builtin_inff();
   const f3 lo = mk(wave_min_all(sec ? o.x : inf), wave_min_all(sec ? o.y : inf), wave_min_all(sec ? o.z : inf));
@@ -786,13 +819,18 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
   spheres_first(sc, pc, sec, o, d, c);
   float best_k = c.t * kOnePlus;
   const uint32_t lane = threadIdx.x & 63;
+  // cooperative tiles: 64-triangle chunk j of the scan (numbered across meshes) goes to wave j mod W
+  const uint32_t cw = __builtin_amdgcn_readfirstlane(co.w);
+  uint32_t chunk0 = 0;
   for (int m = 0; m < pc.num_meshes; ++m) {
     const hrt_mesh& mesh = sc.meshes[m];
     const bool pass = sec && aabb_pass(mesh, o, d);
     if (sec) tests += pass ? mesh.len : 0u;
-    if (!__any(pass)) continue;
     const uint32_t k0 = mesh.first_index, k1 = k0 + mesh.len;
-    for (uint32_t base_v = k0; base_v < k1; base_v += 64) {
+    const uint32_t skip = (cw + co.W - chunk0 % co.W) % co.W;  // this wave's first chunk of the mesh
+    chunk0 += (mesh.len + 63) / 64;
+    if (!__any(pass)) continue;
+    for (uint32_t base_v = k0 + 64 * skip; base_v < k1; base_v += 64 * co.W) {
       const uint32_t base = __builtin_amdgcn_readfirstlane(base_v);  // uniform: scalar survivor indices
       const uint32_t k = base + lane;
       bool keep = false;
@@ -810,26 +848,28 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
         keep = !(s1 | r1);
       }
       unsigned long long mask = __ballot(keep);
+      co.work += 1u + (uint32_t)__popcll(mask);  // one unit per chunk culled and per survivor tested
       if (D && P.diag) {
         dg.sec_considered += min(64u, k1 - base);
         dg.sec_survivors += (uint32_t)__popcll(mask);
       }
       while (mask) {
         // wave-uniform by construction (global source: constant address space -> s_load)
-        const uint32_t kk = __builtin_amdgcn_readfirstlane(base + (uint32_t)__builtin_ctzll(mask));
+        const uint32_t k1 = __builtin_amdgcn_readfirstlane(base + (uint32_t)__builtin_ctzll(mask));
         mask &= mask - 1ull;
         float4 A, B, C, N;
-        src.uniform(kk, A, B, C, N);
+        src.uniform(k1, A, B, C, N);
         if (D && P.diag && pass) {  // how far the two-stage test gets for this survivor
           const f3 ao = o - mk(A.x, A.y, A.z);
           const bool s2 = dot(ao, mk(N.x, N.y, N.z)) > 0.0f;
           dg.sec_stage2 += __any(s2) ? 1u : 0u;
           dg.sec_front += __any(s2 && dot(d, mk(N.x, N.y, N.z)) < 0.0f) ? 1u : 0u;
         }
-        tri_two_stage(A, B, C, N, kk, (uint32_t)m, o, d, c, best_k, pass);
+        tri_two_stage(A, B, C, N, k1, (uint32_t)m, o, d, c, best_k, pass);
       }
     }
   }
+  if (co.W > 1) coop_merge(co, c);
 }
 
 // ---- BUNDLE_BVH: per-lane hierarchy traversal for bounce segments ----------------------------------
@@ -1073,7 +1113,7 @@ enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2 };
 
 template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, const CullSrc& csrc,
-                                                  const BvhSrc& bsrc = BvhSrc{}, uint32_t* list_lds = nullptr) {
+                                                  const BvhSrc& bsrc, uint32_t* list_lds, Coop& co) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
   const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
@@ -1081,6 +1121,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   uint32_t segs = 0, tests = 0;
   const bool active = x < pc.width && lr < P.local_rows && y < pc.height;
   const uint32_t id = active ? x + y * pc.width : 0u;
+  const uint64_t tile_t0 = (D && P.tile_cycles) ? __builtin_readcyclecounter() : 0;
   f3 colour = mk(0.0f, 0.0f, 0.0f);
   uint32_t state = pc.rng_offset * 719393u + id;
   f3 centre = mk(0.0f, 0.0f, 0.0f);
@@ -1119,6 +1160,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
       dg.sec_lanes += run_sec ? nwait : 0u;
       t0 = __builtin_readcyclecounter();
     }
+    if (co.w == 0) co.work += 2u + (any_prim ? 1u + (tl.ok ? tl.n : 64u) : 0u);  // shading, primary list
     if (any_prim) {
       if (tl.ok) {
         world_hit_tile(sc, P, tl, prim, p.pos, p.dir, tests, c);
@@ -1135,7 +1177,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
       if constexpr (Bounce == kBounceBvh) {
         world_hit_bounce_bvh<D>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
       } else if constexpr (Bounce == kBounceCull) {
-        world_hit_bounce_cull<D>(sc, P, csrc, sec, p.pos, p.dir, tests, c, dg);
+        world_hit_bounce_cull<D>(sc, P, csrc, sec, p.pos, p.dir, tests, c, dg, co);
       } else {
         if (sec) c = world_hit_brute(sc, src, pc, p.pos, p.dir, tests);
       }
@@ -1157,11 +1199,20 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
       dg.cyc_shade += t3 - t2;
     }
   }
+  if (co.w != 0) return;  // cooperative tile: wave 0 of the group writes the results
   if (active) {
     colour = colour / (float)pc.num_samples;
     store_pixel(P, x, lr, colour);
   }
   flush_counters(P, segs, tests);
+  if (D && P.tile_cycles && (threadIdx.x & 63) == 0) {  // lane 0 sits at the tile's (0, 0)
+    const uint32_t tiles_x = (pc.width + 7) / 8;
+    unsigned long long* rec = P.tile_cycles + 4 * ((lr / 8) * tiles_x + x / 8);
+    atomicMax(&rec[0], (unsigned long long)(__builtin_readcyclecounter() - tile_t0));  // slowest item of a split tile
+    atomicAdd(&rec[1], (unsigned long long)dg.sec_iters);
+    atomicAdd(&rec[2], (unsigned long long)dg.sec_survivors);
+    atomicAdd(&rec[3], (unsigned long long)dg.cyc_sec);
+  }
   if (P.diag && (threadIdx.x & 63) == 0) {
     atomicAdd(&P.diag[10], (unsigned long long)dg.cyc_prim);
     atomicAdd(&P.diag[11], (unsigned long long)dg.cyc_sec);
@@ -1191,8 +1242,9 @@ __global__ __launch_bounds__(256) void trace_bundle(TraceParams P) {
   uint32_t x, lr;
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
+  Coop solo{0u, 1u, nullptr, 0u, 0u};
   trace_fused_split<kBounceBrute, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhGlobal{},
-                                     lists + (threadIdx.x >> 6) * kTileCapLds);
+                                     lists + (threadIdx.x >> 6) * kTileCapLds, solo);
 }
 
 #ifndef HRT_CULL_WAVES
@@ -1205,8 +1257,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HRT_CULL_WA
   uint32_t x, lr;
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
+  Coop solo{0u, 1u, nullptr, 0u, 0u};
   trace_fused_split<kBounceCull, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhGlobal{},
-                                    lists + (threadIdx.x >> 6) * kTileCapLds);
+                                    lists + (threadIdx.x >> 6) * kTileCapLds, solo);
 }
 
 template <bool D>
@@ -1215,8 +1268,9 @@ __global__ __launch_bounds__(256) void trace_bundle_bvh(TraceParams P) {
   uint32_t x, lr;
   lane_pixel(P, x, lr);
   const float4* T = reinterpret_cast<const float4*>(P.tris);
+  Coop solo{0u, 1u, nullptr, 0u, 0u};
   trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhGlobal{P.bvh_nodes, P.bvh_prims},
-                                   lists + (threadIdx.x >> 6) * kTileCapLds);
+                                   lists + (threadIdx.x >> 6) * kTileCapLds, solo);
 }
 
 
@@ -1238,17 +1292,147 @@ __device__ __forceinline__ void stage_tris(const TraceParams& P, float4* dst, ui
 // the scene staged once) and each wave takes 8x8 pixel tiles from a global counter until the image
 // is done, so no wave idles while a slower wave of its workgroup finishes.  Every wave leaves the
 // loop once the counter passes the tile count.
-template <class Body>
-__device__ __forceinline__ void tile_loop(const TraceParams& P, Body&& body) {
+//
+// Work items (P.items, built by plan_fill from the previous trace's per-tile costs): tile | sub << 25.
+// sub == 0 is a whole tile; sub = 1..K covers rows [(sub-1) * 8/K, sub * 8/K) of a heavy tile with
+// 64/K lanes (the rest idle).  A heavy tile's pixels run as K shorter sample chains in parallel
+// with lighter batches, and the planner puts them first.  Every pixel is computed exactly once and
+// independently of which wave runs it, so the bytes do not depend on the plan.  Each item's cost goes
+// to P.tile_cost[tile] for the next plan: deterministic work units (Coop::work: survivor tests,
+// culled chunks, primary list entries, iterations; the same with or without cooperation) in
+// BUNDLE_CULL_LDS, shader clocks / 16 in BUNDLE_BVH_LDS.
+template <int BLOCK, bool CoopOk, class Body>
+__device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long long* ex, uint32_t* s_item, Body&& body) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t tiles_x = (P.pc.width + 7) / 8, tiles = tiles_x * ((P.local_rows + 7) / 8);
+  const uint32_t n = P.items ? P.sched[1] : tiles;
+  uint32_t first = 0;
+  // Phase 1 (a plan with cooperative heavy tiles): the workgroup takes the heavy items [0, H) one
+  // at a time, all its waves on the same tile (Coop).  The item index goes through LDS; at the loop
+  // head each wave's lane 0 publishes its share of the previous tile's work units.
+  if (CoopOk && P.items && P.coop) {
+    const uint32_t H = P.sched[2];
+    first = H;
+    Coop co{threadIdx.x >> 6, (uint32_t)BLOCK / 64, ex, 0u, 0u};
+    uint32_t prev_tile = 0xFFFFFFFFu, prev_cost = 0;
+    for (;;) {
+      if (lane == 0) {
+        if (prev_tile != 0xFFFFFFFFu) {
+          atomicAdd(&P.tile_cost[prev_tile], prev_cost);
+          atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)prev_cost);
+        }
+        if (threadIdx.x == 0) *s_item = atomicAdd(&P.sched[5], 1u);
+      }
+      __syncthreads();
+      const uint32_t h = __builtin_amdgcn_readfirstlane(*s_item);
+      __syncthreads();
+      if (h >= H) break;
+      const uint32_t tile = __builtin_amdgcn_readfirstlane(P.items[h]) & 0x01FFFFFFu;
+      const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+      co.work = 0;
+      body(tx * 8 + (lane & 7), ty * 8 + (lane >> 3), co);
+      prev_cost = __builtin_amdgcn_readfirstlane(co.work);
+      prev_tile = tile;
+    }
+    if (lane == 0 && prev_tile != 0xFFFFFFFFu) {
+      atomicAdd(&P.tile_cost[prev_tile], prev_cost);
+      atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)prev_cost);
+    }
+  }
+  // Phase 2: every wave on its own.  The loop's only lane-divergent block is at its head (lane 0
+  // publishes the previous item's cost and takes the next item).  A second lane-0 block at the latch
+  // let the compiler thread lanes 1-63 straight back to the body past the head, where they spun on
+  // a stale item: keep it this way.
+  Coop solo{0u, 1u, nullptr, 0u, 0u};
+  uint32_t prev_tile = 0xFFFFFFFFu, prev_cost = 0;
   for (;;) {
     uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(P.tile_counter, 1u);
+    if (lane == 0) {
+      if (prev_tile != 0xFFFFFFFFu) {
+        atomicAdd(&P.tile_cost[prev_tile], prev_cost);
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)prev_cost);
+      }
+      t = first + atomicAdd(&P.sched[0], 1u);
+    }
     t = __builtin_amdgcn_readfirstlane(t);
-    if (t >= tiles) break;
-    const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
-    body(tx * 8 + (lane & 7), ty * 8 + (lane >> 3));
+    if (t >= n) break;
+    const uint32_t item = __builtin_amdgcn_readfirstlane(P.items ? P.items[t] : t);
+    const uint32_t tile = item & 0x01FFFFFFu, sub = (item >> 25) & 15u;
+    const bool hot = item >> 31;  // heavy last time: issue priority over the light tiles' waves
+    const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+    uint32_t x = tx * 8 + (lane & 7), lr = ty * 8 + (lane >> 3);
+    if (sub) {
+      const uint32_t rows = 8 / P.split_k, r = lane >> 3;
+      if (r < rows)
+        lr = ty * 8 + (sub - 1) * rows + r;
+      else
+        x = 0xFFFFFFFFu;  // idle lane
+    }
+    const uint64_t t0 = __builtin_readcyclecounter();
+    if (hot) __builtin_amdgcn_s_setprio(3);
+    solo.work = 0;
+    body(x, lr, solo);
+    if (hot) __builtin_amdgcn_s_setprio(0);
+    // cost: the work count where the body keeps one (BUNDLE_CULL_LDS), else shader clocks / 16
+    const uint64_t c = CoopOk ? (uint64_t)solo.work : (__builtin_readcyclecounter() - t0) >> 4;
+    prev_cost = __builtin_amdgcn_readfirstlane(c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c);
+    prev_tile = tile;
+  }
+  if (lane == 0 && prev_tile != 0xFFFFFFFFu) {
+    atomicAdd(&P.tile_cost[prev_tile], prev_cost);
+    atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)prev_cost);
+  }
+}
+
+// Planner (after a trace of an LDS variant, before the next).  Items go in decreasing order of the
+// tile's last cost (longest first: a long tile started late is what sets a frame's end), by a
+// 64-bucket half-octave histogram and a descending scan; heavy tiles are the top buckets, k items
+// each: cost >= factor x (sum of costs / resident waves), to the bucket, i.e. a tile that alone
+// would take `factor` times a wave's fair share of the frame.  sched[8..71] histogram, [72..135] bucket offsets,
+// [136..199] bucket cursors, [3] first heavy bucket.
+constexpr uint32_t kPlanBuckets = 64;
+__device__ __forceinline__ uint32_t cost_bucket(unsigned long long c) {
+  if (c < 2) return 0;
+  if (c > 0xFFFFFFFFull) return kPlanBuckets;
+  const uint32_t v = (uint32_t)c, l = 31 - __clz(v);  // floor(log2 c) >= 1
+  return min(2 * l + ((v >> (l - 1)) & 1u), kPlanBuckets - 1);
+}
+__global__ __launch_bounds__(256) void plan_hist(uint32_t* sched, const uint32_t* cost, uint32_t tiles) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < tiles) atomicAdd(&sched[8 + cost_bucket(cost[i])], 1u);
+}
+__global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves, uint32_t factor, uint32_t k,
+                                                uint32_t prio) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long sum = *reinterpret_cast<const unsigned long long*>(sched + 6);
+  const uint32_t hb = cost_bucket((unsigned long long)factor * sum / (waves ? waves : 1u));
+  uint32_t pos = 0, heavy = 0;
+  for (int b = (int)kPlanBuckets - 1; b >= 0; --b) {
+    const uint32_t cnt = sched[8 + b], hv = (uint32_t)b >= hb;
+    sched[72 + b] = pos;
+    pos += cnt * (hv ? k : 1u);
+    heavy += hv ? cnt : 0u;
+  }
+  sched[1] = prio > 1 ? heavy * k : pos;  // prio 2: heavy items only (diagnostics)
+  sched[2] = heavy;
+  sched[3] = hb;
+}
+__global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t* cost, uint32_t tiles, uint32_t k,
+                                                 uint32_t prio, uint32_t* items) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= tiles) return;
+  const uint32_t b = cost_bucket(cost[i]);
+  const bool heavy = b >= sched[3];
+  const uint32_t slot = heavy ? k : 1u;
+  const uint32_t at = sched[72 + b] + atomicAdd(&sched[136 + b], slot);
+  if (!heavy) {
+    items[at] = i;
+  } else {
+    const uint32_t flag = prio ? 0x80000000u : 0u;
+    if (k == 1)
+      items[at] = i | flag;
+    else
+      for (uint32_t s = 0; s < k; ++s) items[at + s] = i | ((s + 1) << 25) | flag;
   }
 }
 
@@ -1256,9 +1440,15 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, Body&& body) {
 // latency).  Dynamic LDS: n_tris x 48 B triangles.
 template <int BLOCK, bool D>
 __global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
+  __shared__ uint32_t s_item;
   stage_tris(P, lds_tris, BLOCK);
+  // cooperative-tile exchange slots (Coop) after the triangle image, all clear
+  unsigned long long* ex = reinterpret_cast<unsigned long long*>(lds_tris + 3 * P.n_tris);
+  for (uint32_t k = threadIdx.x; k < 3 * 64; k += BLOCK) ex[k] = ~0ull;
   __syncthreads();
-  tile_loop(P, [&](uint32_t x, uint32_t lr) { trace_fused_split<kBounceCull, D>(P, x, lr, CullLds{lds_tris}); });
+  tile_loop<BLOCK, true>(P, ex, &s_item, [&](uint32_t x, uint32_t lr, Coop& co) {
+    trace_fused_split<kBounceCull, D>(P, x, lr, CullLds{lds_tris}, BvhGlobal{}, nullptr, co);
+  });
 }
 
 // BUNDLE_BVH with the hierarchy and the triangle image in LDS (persistent 1024-thread workgroups).
@@ -1275,8 +1465,9 @@ __global__ __launch_bounds__(1024) void trace_bundle_bvh_lds(TraceParams P) {
   for (uint32_t k = threadIdx.x; k < nm; k += 1024) kbase[k] = P.bvh_keybase[k];
   __syncthreads();
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  tile_loop(P, [&](uint32_t x, uint32_t lr) {
-    trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhLds{nodes, lds_tris, entries, kbase});
+  tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co) {
+    trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhLds{nodes, lds_tris, entries, kbase},
+                                     nullptr, co);
   });
 }
 
@@ -1415,7 +1606,7 @@ __global__ __launch_bounds__(256) void f32_to_rgba8(const float4* src, uint32_t*
 namespace hrt {
 
 static inline unsigned blocks_for(size_t n) { return (unsigned)((n + 255) / 256); }
-constexpr size_t kMaxLdsScene = 160 * 1024;
+constexpr size_t kMaxLdsScene = 160 * 1024 - 64;  // dynamic LDS per CU, leaving room for the kernels' static LDS
 constexpr uint32_t kAutoCullTris = 256;   // BUNDLE_CULL from this many mesh triangles, BUNDLE below
 constexpr uint32_t kAutoBvhTris = 4096;   // BUNDLE_BVH from this many (profiles/r01d_bvh_scaling.log)
 
@@ -1427,8 +1618,9 @@ bool bvh_lds_fits(const TraceParams& p) { return p.bvh_nodes && p.bvh_entries &&
 
 // BUNDLE_CULL_LDS workgroup size for a scene of n triangles (0 = does not fit): two 512-thread
 // workgroups per CU when twice the footprint fits the 160 KiB, else one of 1024.
+constexpr size_t kCoopLds = 3 * 64 * 8;  // cooperative-tile exchange slots
 uint32_t lds_block(uint32_t n) {
-  const size_t tri = (size_t)n * 48;
+  const size_t tri = (size_t)n * 48 + kCoopLds;
   return tri <= kMaxLdsScene / 2 ? 512u : tri <= kMaxLdsScene ? 1024u : 0u;
 }
 
@@ -1449,6 +1641,28 @@ int resolve_variant(const TraceParams& p, int variant) {
   return variant;
 }
 
+// Persistent kernels: plan this trace from the last one's tile costs (when p.plan_valid and
+// splitting is on), then reset the counters the trace fills.  q.items = nullptr: plain tile order.
+static hipError_t prepare_schedule(TraceParams& q, hipStream_t stream) {
+  const uint32_t tiles = ((q.pc.width + 7) / 8) * ((q.local_rows + 7) / 8);
+  const bool plan = q.plan_valid && tiles > 0;  // longest-first order whenever last trace's costs are known
+  q.items = plan ? q.item_buf : nullptr;
+  hipError_t e;
+  if (plan) {
+    if ((e = hipMemsetAsync(q.sched + 8, 0, 192 * 4, stream)) != hipSuccess) return e;  // histogram, cursors
+    plan_hist<<<(tiles + 255) / 256, 256, 0, stream>>>(q.sched, q.tile_cost, tiles);
+    // factor auto (-1): 3 when a resident wave gets more than 4 tiles, else 1 (profiles/r01k_schedule_sweep)
+    const uint32_t waves = q.num_cus * 16u;
+    const uint32_t factor = q.split_factor >= 0 ? (uint32_t)q.split_factor : tiles > 4 * waves ? 3u : 1u;
+    plan_scan<<<1, 64, 0, stream>>>(q.sched, waves, factor, q.split_k, q.split_prio);
+    plan_fill<<<(tiles + 255) / 256, 256, 0, stream>>>(q.sched, q.tile_cost, tiles, q.split_k, q.split_prio,
+                                                       q.item_buf);
+  }
+  if ((e = hipMemsetAsync(q.tile_cost, 0, (size_t)tiles * 4, stream)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(q.sched + 5, 0, 12, stream)) != hipSuccess) return e;  // coop counter, cost sum
+  return hipMemsetAsync(q.sched, 0, 4, stream);
+}
+
 hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, int* ran, int* block_out) {
   static bool lds_attr = false;
   if (!lds_attr) {
@@ -1465,6 +1679,7 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kMaxLdsScene / 2));
     for (const void* f : whole_cu)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
+    (void)hipGetLastError();  // a refused attribute shows up as a launch failure of that kernel, not here
   }
   variant = resolve_variant(p, variant);
   *ran = variant;
@@ -1481,9 +1696,10 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
     }
     case HRT_KERNEL_BUNDLE_BVH_LDS: {
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
-      const TraceParams& q = p;
+      TraceParams q = p;
+      q.coop = 0;
       const size_t lds = bvh_lds_bytes(p);
-      if (hipError_t e = hipMemsetAsync(p.tile_counter, 0, 4, stream); e != hipSuccess) return e;
+      if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
       if (p.diag)
         trace_bundle_bvh_lds<true><<<p.num_cus, 1024, lds, stream>>>(q);
       else
@@ -1493,11 +1709,12 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
     }
     case HRT_KERNEL_BUNDLE_CULL_LDS: {
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
-      const TraceParams& q = p;
+      TraceParams q = p;
       const uint32_t block = lds_block(p.n_tris);
       *block_out = (int)block;
-      const size_t lds = (size_t)p.n_tris * 48;
-      if (hipError_t e = hipMemsetAsync(p.tile_counter, 0, 4, stream); e != hipSuccess) return e;
+      const size_t lds = (size_t)p.n_tris * 48 + kCoopLds;
+      q.coop = p.coop && p.split_k == 1 && p.pc.num_meshes <= 62 ? 1u : 0u;
+      if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
       if (block == 512) {
         if (p.diag)
           trace_bundle_cull_lds<512, true><<<2 * p.num_cus, 512, lds, stream>>>(q);

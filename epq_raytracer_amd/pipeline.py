@@ -179,6 +179,14 @@ class HrtContext:
         self._check(self.lib.hrt_get_diagnostics(self.handle, _lib.ptr(out), len(out)), "hrt_get_diagnostics")
         return dict(zip(_lib.DIAG_NAMES, (int(v) for v in out)))
 
+    def tile_profile(self) -> np.ndarray:
+        """Per 8x8 tile of the last trace, (ceil(local_rows/8), ceil(W/8), 4): shader clocks, bounce
+        iterations, bounce survivor tests, bounce clocks (needs OPT_COUNTERS=2)."""
+        ty, tx = (self.local_rows + 7) // 8, (self.width + 7) // 8
+        out = np.zeros(ty * tx * 4, np.uint64)
+        self._check(self.lib.hrt_get_tile_profile(self.handle, _lib.ptr(out), len(out)), "hrt_get_tile_profile")
+        return out.reshape(ty, tx, 4)
+
     def scene_info(self) -> dict:
         """What the last set_scene built for the BVH kernel (hrt_get_scene_info)."""
         out = np.zeros(len(_lib.SCENE_INFO_NAMES), np.uint32)

@@ -179,7 +179,23 @@ typedef enum hrt_option {
    * or when no lane has a primary segment left (1..64, default 48; results do not depend on it) */
   HRT_OPT_SECONDARY_BATCH = 3,
   /* BUNDLE_BVH: triangles per leaf of the hierarchy the next hrt_set_scene builds (1..16, default 4) */
-  HRT_OPT_BVH_LEAF_SIZE = 4
+  HRT_OPT_BVH_LEAF_SIZE = 4,
+  /* persistent (*_LDS) kernels: a tile that took more than 4x the mean in the previous trace runs as
+   * this many work items of 8/k rows each, scheduled first (1 = off; 2, 4 default, 8).  The frame's
+   * time is set by its slowest tiles' sample chains; results do not depend on it. */
+  HRT_OPT_SPLIT = 5,
+  /* heavy tile: its cost in the previous trace exceeds this multiple of a resident wave's fair share
+   * (sum of tile costs / resident waves), to a half octave (0: every tile is heavy; default -1 =
+   * auto: 3 when there are more than 4 tiles per resident wave, else 1) */
+  HRT_OPT_SPLIT_FACTOR = 6,
+  /* persistent kernels: heavy tiles (as above) run at raised wave issue priority (1 default, 0 off;
+   * 2 = diagnostics: a planned trace runs ONLY the heavy tiles, the frame is incomplete) */
+  HRT_OPT_PRIORITY = 7,
+  /* persistent kernels: launch workgroups for at most this many CUs (0 = all; latency experiments) */
+  HRT_OPT_GRID_CUS = 8,
+  /* BUNDLE_CULL_LDS with HRT_OPT_SPLIT = 1: heavy tiles run cooperatively, every wave of a workgroup
+   * on the same tile with the bounce cull's chunks dealt out over the waves (1 default, 0 off) */
+  HRT_OPT_COOP = 9
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */
@@ -245,6 +261,11 @@ hrt_status hrt_synchronize(hrt_context* ctx);
 hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out); /* synchronizes */
 hrt_status hrt_reset_stats(hrt_context* ctx);
 hrt_status hrt_get_diagnostics(hrt_context* ctx, uint64_t* out, uint32_t count); /* synchronizes */
+/* Diagnostics (HRT_OPT_COUNTERS = 2): per 8x8 tile of the last trace, row-major over ceil(W/8) x
+ * ceil(local_rows/8) tiles, 4 values: shader clocks (slowest work item), bounce iterations, bounce
+ * survivor tests, bounce-phase clocks (the frame's critical path is its slowest tile).  count =
+ * values (at most 4 x tiles). */
+hrt_status hrt_get_tile_profile(hrt_context* ctx, uint64_t* out, uint32_t count);
 /* Extension (no reference counterpart): out[i] = hrt_scene_info i for i < count, from the last
  * hrt_set_scene. */
 hrt_status hrt_get_scene_info(hrt_context* ctx, uint32_t* out, uint32_t count);

@@ -53,6 +53,118 @@ def test_every_variant_bit_exact(scene, size, spp, bounces, variant):
     assert (gseg, gtt) == (seg, tt)
 
 
+@pytest.mark.parametrize("split,factor,prio", [(1, 4, 0), (1, 4, 1), (1, 0, 1), (2, 0, 0), (4, 0, 1), (8, 0, 0),
+                                               (4, 4, 1), (8, 2, 1)])
+@pytest.mark.parametrize("scene,size,spp,bounces,variant", [("cave", (64, 48), 2, 8, 7), ("island", (75, 41), 3, 8, 7),
+                                                            ("island", (75, 41), 3, 8, 8)])
+def test_split_schedule_bit_exact(scene, size, spp, bounces, variant, split, factor, prio):
+    """The persistent kernels' second and later traces follow the planner's work items: tiles that
+    cost more than factor x the mean last time run first, as `split` row groups, at raised wave
+    priority when prio (HRT_OPT_SPLIT / _FACTOR / _PRIORITY; factor 0 marks every tile heavy).
+    Every plan gives the oracle's frame and counts."""
+    case = SceneCase(scene, size, spp, bounces)
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context(variant=variant, options={_lib.OPT_SPLIT: split, _lib.OPT_SPLIT_FACTOR: factor,
+                                                 _lib.OPT_PRIORITY: prio})
+    for _ in range(3):  # unplanned, planned from an unsplit trace, planned from a split one
+        ctx.reset_stats()
+        ctx.trace(case.push())
+        st = ctx.stats()
+        img = ctx.read(_lib.IMG_TRACE)
+        assert np.array_equal(img, ref), mismatch_report(img, ref)
+        assert (st.segments, st.tri_tests) == (seg, tt)
+        assert st.last_kernel == variant
+    ctx.close()
+
+
+def _tie_soup(seed=5, n=300):
+    """Exact ties across the cooperative waves' chunks: a triangle soup stored twice in one mesh
+    (triangle i and i + n tie; their 64-triangle chunks go to different waves) and again as a second
+    mesh (ties across meshes), plus a mirror sphere and a light sphere."""
+    rng = np.random.default_rng(seed)
+    a = rng.uniform(-4, 4, (n, 3))
+    v = np.concatenate([a[:, None, :], (a + rng.uniform(-1.5, 1.5, (n, 3)))[:, None, :],
+                        (a + rng.uniform(-1.5, 1.5, (n, 3)))[:, None, :]], 1).reshape(-1, 3)
+    v = np.concatenate([v, v]).astype(np.float32)
+    mesh = E.Mesh(v, np.arange(len(v), dtype=np.uint32))
+    st = E.RayTracerSettings(num_samples=3, max_bounces=8, use_environment_lighting=True,
+                             sphere_data=[E.Sphere([0.0, 0.0, 0.0], 1.0, E.MetalMaterial([0.9, 0.9, 0.9], 1.0, 0.0))],
+                             mesh_data=[E.RayTracingMesh(mesh, E.LambertianMaterial([0.8, 0.7, 0.6])),
+                                        E.RayTracingMesh(E.Mesh(v.copy(), np.arange(len(v), dtype=np.uint32)),
+                                                         E.MetalMaterial([0.6, 0.7, 0.9], 0.8, 0.1))])
+    return SceneCase(settings=st, camera=E.Camera([0.3, 0.2, -9.0], [0.0, 0.0, 1.0]), size=(72, 56),
+                     num_samples=3, max_bounces=8)
+
+
+@pytest.mark.parametrize("factor", [0, 4, -1])
+@pytest.mark.parametrize("scene", ["island", "cave", "box", "spheres", "ties"])
+def test_coop_tiles_bit_exact(scene, factor):
+    """Cooperative heavy tiles (HRT_OPT_COOP, BUNDLE_CULL_LDS): after the first trace the tiles that
+    cost more than factor x the mean (factor 0: every tile) run with all waves of a workgroup, the
+    bounce cull dealt out over the waves and the closest hits merged by (t, scan order)."""
+    sizes = {"island": (75, 41, 3), "cave": (64, 48, 2), "box": (45, 33, 3), "spheres": (40, 30, 2)}
+    if scene == "ties":
+        case = _tie_soup()
+    else:
+        w, h, spp = sizes[scene]
+        case = SceneCase(scene, (w, h), spp, 8)
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context(variant=7, options={_lib.OPT_SPLIT: 1, _lib.OPT_SPLIT_FACTOR: factor, _lib.OPT_COOP: 1})
+    for _ in range(3):
+        ctx.reset_stats()
+        ctx.trace(case.push())
+        st = ctx.stats()
+        img = ctx.read(_lib.IMG_TRACE)
+        assert np.array_equal(img, ref), mismatch_report(img, ref)
+        assert (st.segments, st.tri_tests) == (seg, tt)
+        assert st.last_kernel == 7
+    ctx.close()
+
+
+@pytest.mark.parametrize("split,coop", [(8, 0), (1, 1)])
+def test_split_schedule_partition_and_scene_change(split, coop):
+    """Ragged row-tile partition (local rows not a multiple of 8) with every tile split (or run
+    cooperatively), and a scene switch in between (the old costs are dropped)."""
+    case = SceneCase("island", (80, 70), 2, 8)
+    ctx = case.context(partition=(4, 1, 3), variant=7,
+                       options={_lib.OPT_SPLIT: split, _lib.OPT_SPLIT_FACTOR: 0, _lib.OPT_COOP: coop})
+    ctx.trace(case.push())
+    first = ctx.read(_lib.IMG_TRACE)
+    s1 = ctx.stats()
+    for _ in range(2):
+        ctx.reset_stats()
+        ctx.trace(case.push())
+        assert np.array_equal(ctx.read(_lib.IMG_TRACE), first)
+        s = ctx.stats()
+        assert (s.segments, s.tri_tests) == (s1.segments, s1.tri_tests)
+    ctx.set_scene(case.rays, case.spheres, case.tris, case.meshes)
+    ctx.trace(case.push())
+    assert np.array_equal(ctx.read(_lib.IMG_TRACE), first)
+    ctx.close()
+    # the partition's rows are the oracle's rows
+    from epq_raytracer_amd import rowtiles
+    ref, _, _, _ = case.oracle()
+    rows = rowtiles.global_rows(70, 4, 3, 1)
+    valid = rows < 70
+    assert np.array_equal(first[valid], ref[rows[valid]])
+
+
+def test_split_options_validated():
+    case = SceneCase("box", (16, 16), 1, 1)
+    ctx = case.context(variant=7)
+    for bad in (0, 3, 16):
+        with pytest.raises(Exception):
+            ctx.set_option(_lib.OPT_SPLIT, bad)
+    with pytest.raises(Exception):
+        ctx.set_option(_lib.OPT_PRIORITY, 3)
+    with pytest.raises(Exception):
+        ctx.set_option(_lib.OPT_COOP, 2)
+    with pytest.raises(Exception):
+        ctx.set_option(_lib.OPT_SPLIT_FACTOR, -2)
+    ctx.set_option(_lib.OPT_SPLIT_FACTOR, -1)
+    ctx.close()
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_rgba32f_mode_bitwise(variant):
     case = SceneCase("island", (96, 54), 4, 8)

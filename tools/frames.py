@@ -1,0 +1,45 @@
+"""Frame-to-frame stability of the persistent kernels' schedule: N consecutive traces of one
+configuration, each planned from the previous one's tile costs.
+
+    python tools/frames.py [--scene island --variant 0 --frames 12 --partition 16,0,8 --coop 1 --factor -1]"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
+
+from helpers import SceneCase, _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="island")
+    ap.add_argument("--size", default="1920x1080")
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--frames", type=int, default=12)
+    ap.add_argument("--partition", default=None)
+    ap.add_argument("--coop", type=int, default=1)
+    ap.add_argument("--factor", type=int, default=-1)
+    ap.add_argument("--prio", type=int, default=1)
+    a = ap.parse_args()
+    W, H = (int(v) for v in a.size.split("x"))
+    case = SceneCase(a.scene, (W, H), a.spp, a.bounces)
+    part = tuple(int(v) for v in a.partition.split(",")) if a.partition else None
+    ctx = case.context(variant=a.variant, partition=part,
+                       options={_lib.OPT_COOP: a.coop, _lib.OPT_SPLIT_FACTOR: a.factor, _lib.OPT_PRIORITY: a.prio})
+    pc = case.push(1)
+    ms = []
+    for _ in range(a.frames):
+        ctx.reset_stats()
+        ctx.trace(pc)
+        ms.append(round(ctx.stats().total_trace_ms, 3))
+    ctx.close()
+    print(json.dumps({"scene": a.scene, "partition": a.partition, "coop": a.coop, "factor": a.factor, "ms": ms}))
+
+
+if __name__ == "__main__":
+    main()

@@ -31,11 +31,18 @@ def main():
     ap.add_argument("--no-ref", action="store_true", help="skip the literal-kernel reference frame")
     ap.add_argument("--diag", action="store_true", help="also print the bundle kernels' cull diagnostics")
     ap.add_argument("--sec-batch", type=int, nargs="+", default=[48], help="HRT_OPT_SECONDARY_BATCH values to sweep")
+    ap.add_argument("--split", type=int, nargs="+", default=[1], help="HRT_OPT_SPLIT values to sweep (LDS variants)")
+    ap.add_argument("--prio", type=int, nargs="+", default=[1], help="HRT_OPT_PRIORITY values to sweep")
+    ap.add_argument("--factor", type=int, nargs="+", default=[-1], help="HRT_OPT_SPLIT_FACTOR values to sweep")
+    ap.add_argument("--coop", type=int, nargs="+", default=[1], help="HRT_OPT_COOP values to sweep")
     ap.add_argument("--leaf", type=int, default=None, help="HRT_OPT_BVH_LEAF_SIZE for the scene build")
+    ap.add_argument("--partition", default=None,
+                    help="TILE,INDEX,COUNT: trace only one rank's row tiles (what each GPU does at N > 1)")
     a = ap.parse_args()
     W, H = (int(v) for v in a.size.split("x"))
     case = SceneCase(a.scene, (W, H), a.spp, a.bounces)
-    ctx = case.context(options={_lib.OPT_BVH_LEAF_SIZE: a.leaf} if a.leaf else None)
+    part = tuple(int(v) for v in a.partition.split(",")) if a.partition else None
+    ctx = case.context(options={_lib.OPT_BVH_LEAF_SIZE: a.leaf} if a.leaf else None, partition=part)
     print(json.dumps({"scene_info": ctx.scene_info()}), flush=True)
     pc = case.push(1)
     # warm up + reference image (literal kernel), unless profiling one variant alone
@@ -44,21 +51,29 @@ def main():
         ctx.set_option(_lib.OPT_KERNEL_VARIANT, 1)
         ctx.trace(pc)
         ref = ctx.read(_lib.IMG_TRACE)
-    combos = [(v, sb) for v in a.variants for sb in (a.sec_batch if v in (0, 4, 5, 6, 7, 8) else [a.sec_batch[0]])]
+    combos = [(v, sb, k) for v in a.variants for sb in (a.sec_batch if v in (0, 4, 5, 6, 7, 8) else [a.sec_batch[0]])
+              for k in ([(k, p, f, c) for k in a.split for p in a.prio for f in a.factor for c in a.coop]
+                        if v in (0, 7, 8) else [(a.split[0], a.prio[0], a.factor[0], a.coop[0])])]
     res = {vs: [] for vs in combos}
     stats = {}
     same = {}
-    for r in range(a.rounds):
-        for v, sb in combos:
+    for v, sb, k in combos:  # each combo's traces back to back: the schedule plans from its own last trace
+        for r in range(-1, a.rounds):
             ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
             ctx.set_option(_lib.OPT_SECONDARY_BATCH, sb)
+            ctx.set_option(_lib.OPT_SPLIT, k[0])
+            ctx.set_option(_lib.OPT_PRIORITY, k[1])
+            ctx.set_option(_lib.OPT_SPLIT_FACTOR, k[2])
+            ctx.set_option(_lib.OPT_COOP, k[3])
             ctx.reset_stats()
             ctx.trace(pc)
             st = ctx.stats()
-            res[(v, sb)].append(st.total_trace_ms)
-            stats[(v, sb)] = (st.segments, st.tri_tests, st.wave_steps)
+            if r < 0:
+                continue  # warm-up: this combo's tile costs for the planner
+            res[(v, sb, k)].append(st.total_trace_ms)
+            stats[(v, sb, k)] = (st.segments, st.tri_tests, st.wave_steps)
             if r == 0:
-                same[(v, sb)] = None if ref is None else bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
+                same[(v, sb, k)] = None if ref is None else bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
     if a.diag:
         for v in a.variants:
             if v in (0, 4, 5, 6, 7, 8):
@@ -87,14 +102,14 @@ def main():
                 print(json.dumps(d), flush=True)
                 ctx.set_option(_lib.OPT_COUNTERS, 1)
     out = []
-    for v, sb in combos:
-        ms = np.array(res[(v, sb)])
-        seg, tt, ws = stats[(v, sb)]
+    for v, sb, k in combos:
+        ms = np.array(res[(v, sb, k)])
+        seg, tt, ws = stats[(v, sb, k)]
         med = float(np.median(ms))
-        row = {"variant": v, "sec_batch": sb, "ms_median": round(med, 3), "ms_min": round(float(ms.min()), 3),
+        row = {"variant": v, "sec_batch": sb, "split": k[0], "prio": k[1], "factor": k[2], "coop": k[3], "ms_median": round(med, 3), "ms_min": round(float(ms.min()), 3),
                "mrays_s": round(seg / med / 1e3, 1), "tflops_alg": round(38 * tt / med / 1e9, 2),
                "lane_eff": round(seg / max(64 * ws, 1), 4), "segments": seg, "tri_tests": tt,
-               "identical_to_literal": same[(v, sb)]}
+               "identical_to_literal": same[(v, sb, k)]}
         out.append(row)
         print(json.dumps(row), flush=True)
     if a.json:
