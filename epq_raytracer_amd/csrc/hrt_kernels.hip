@@ -1397,9 +1397,16 @@ __device__ __forceinline__ uint32_t cost_bucket(unsigned long long c) {
   const uint32_t v = (uint32_t)c, l = 31 - __clz(v);  // floor(log2 c) >= 1
   return min(2 * l + ((v >> (l - 1)) & 1u), kPlanBuckets - 1);
 }
+// Both passes count in LDS first: a frame's tiles crowd a few buckets, and per-tile global atomics
+// on those few words serialize (0.3 ms per pass at 1080p).
 __global__ __launch_bounds__(256) void plan_hist(uint32_t* sched, const uint32_t* cost, uint32_t tiles) {
+  __shared__ uint32_t h[kPlanBuckets];
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i < tiles) atomicAdd(&sched[8 + cost_bucket(cost[i])], 1u);
+  if (threadIdx.x < kPlanBuckets) h[threadIdx.x] = 0;
+  __syncthreads();
+  if (i < tiles) atomicAdd(&h[cost_bucket(cost[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x < kPlanBuckets && h[threadIdx.x]) atomicAdd(&sched[8 + threadIdx.x], h[threadIdx.x]);
 }
 __global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves, uint32_t factor, uint32_t k,
                                                 uint32_t prio) {
@@ -1419,12 +1426,21 @@ __global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves,
 }
 __global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t* cost, uint32_t tiles, uint32_t k,
                                                  uint32_t prio, uint32_t* items) {
+  __shared__ uint32_t cnt[kPlanBuckets], base[kPlanBuckets];
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= tiles) return;
-  const uint32_t b = cost_bucket(cost[i]);
-  const bool heavy = b >= sched[3];
+  if (threadIdx.x < kPlanBuckets) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t hb = sched[3];
+  const uint32_t b = i < tiles ? cost_bucket(cost[i]) : 0u;
+  const bool heavy = b >= hb;
   const uint32_t slot = heavy ? k : 1u;
-  const uint32_t at = sched[72 + b] + atomicAdd(&sched[136 + b], slot);
+  const uint32_t local = i < tiles ? atomicAdd(&cnt[b], slot) : 0u;
+  __syncthreads();
+  if (threadIdx.x < kPlanBuckets && cnt[threadIdx.x])
+    base[threadIdx.x] = sched[72 + threadIdx.x] + atomicAdd(&sched[136 + threadIdx.x], cnt[threadIdx.x]);
+  __syncthreads();
+  if (i >= tiles) return;
+  const uint32_t at = base[b] + local;
   if (!heavy) {
     items[at] = i;
   } else {
