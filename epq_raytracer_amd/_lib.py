@@ -72,10 +72,10 @@ MODE_RGBA8, MODE_RGBA32F = 0, 1
 IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
-OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP = 5, 6, 7, 8, 9
+OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP, OPT_WQ_NODE_CAP = 5, 6, 7, 8, 9, 10
 # hrt_kernel (include/hip_raytrace.h)
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
-KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS, KERNEL_BUNDLE_BVH_LDS = 6, 7, 8
+KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS, KERNEL_BUNDLE_BVH_LDS, KERNEL_BUNDLE_WQ = 6, 7, 8, 9
 # kernel symbol (as rocprofv3 names it) of a resolved hrt_kernel + workgroup size
 def kernel_symbol(kernel: int, block: int, diag: bool = False) -> str:
     d = "true" if diag else "false"
@@ -83,12 +83,13 @@ def kernel_symbol(kernel: int, block: int, diag: bool = False) -> str:
         return "hrt::" + {1: "trace_literal", 2: "trace_brute", 3: "trace_brute_lds"}[kernel] + "(hrt::TraceParams)"
     if kernel == 7:
         return f"void hrt::trace_bundle_cull_lds<{block}, {d}>(hrt::TraceParams)"
-    name = {4: "trace_bundle", 5: "trace_bundle_cull", 6: "trace_bundle_bvh", 8: "trace_bundle_bvh_lds"}.get(kernel, "?")
+    name = {4: "trace_bundle", 5: "trace_bundle_cull", 6: "trace_bundle_bvh", 8: "trace_bundle_bvh_lds",
+            9: "trace_bundle_wq"}.get(kernel, "?")
     return f"void hrt::{name}<{d}>(hrt::TraceParams)"
 
 
 KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle", 5: "bundle_cull", 6: "bundle_bvh",
-                7: "bundle_cull_lds", 8: "bundle_bvh_lds"}
+                7: "bundle_cull_lds", 8: "bundle_bvh_lds", 9: "bundle_wq"}
 DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounce_iters", "bounce_considered",
               "bounce_survivors", "bounce_lanes", "bvh_visits", "bvh_prim_tests", "bvh_band_tests", "primary_cycles", "bounce_cycles",
               "shade_cycles", "bounce_stage2", "bounce_front", "bvh_trips",

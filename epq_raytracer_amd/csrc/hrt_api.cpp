@@ -63,10 +63,11 @@ struct hrt_context {
   uint32_t* tile_cost = nullptr;  // per 8x8 tile
   uint32_t* item_buf = nullptr;   // planned work items (tiles x 8)
   bool plan_valid = false;        // tile_cost describes the last trace (same size, persistent kernel)
-  uint32_t split_k = 1, split_prio = 1;
+  uint32_t split_k = 0, split_prio = 1;  // split 0: auto (per kernel, launch_trace)
   int32_t split_factor = -1;  // auto
   uint32_t grid_cus = 0;  // HRT_OPT_GRID_CUS (0: every CU)
   uint32_t coop = 1;      // HRT_OPT_COOP
+  uint32_t wq_node_cap = 0;  // HRT_OPT_WQ_NODE_CAP (0 = auto)
   uint32_t num_cus = 0;
   uint32_t* cam_meta = nullptr;   // bundle variants: cam_start[n_meshes], cam_count[n_meshes]
   uint32_t cam_capacity = 0;      // sum of mesh lengths
@@ -82,6 +83,7 @@ struct hrt_context {
   uint32_t bvh_info[HRT_NUM_SCENE_INFO] = {};  // hrt_get_scene_info
   float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f;
   uint32_t bvh_leaf = 4;
+  uint32_t bvh_built_leaf = 4;  // leaf size of the hierarchy the last hrt_set_scene built
 
   int variant = 0;
   bool counters_on = true;
@@ -363,6 +365,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   ctx->bvh_info[3] = bvh.n_never;
   ctx->bvh_info[4] = built ? 1u : 0u;
   ctx->bvh_abs_coef = bvh.abs_coef;
+  ctx->bvh_built_leaf = std::max(1u, std::min(ctx->bvh_leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
   ctx->bvh_rel_t = bvh.rel_t;
   ctx->bvh_info[5] = (uint32_t)(bvh.band_list.size() / 4);
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
@@ -423,6 +426,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.split_factor = ctx->split_factor;
   p.split_prio = ctx->split_prio;
   p.coop = ctx->coop;
+  p.wq_ncap = ctx->wq_node_cap;  // request; launch_trace sizes the stacks
   p.plan_valid = ctx->plan_valid ? 1u : 0u;
   p.num_cus = ctx->grid_cus ? std::min(ctx->grid_cus, ctx->num_cus) : ctx->num_cus;
   p.bvh_nodes = ctx->bvh_info[4] ? ctx->bvh_nodes : nullptr;
@@ -438,6 +442,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.bvh_abs_coef = ctx->bvh_abs_coef;
   p.bvh_rel_t = ctx->bvh_rel_t;
   p.bvh_n_irregular = ctx->bvh_info[2];
+  p.bvh_max_leaf = ctx->bvh_built_leaf;
   const int variant = ctx->variant;
 
   EventPair ev;
@@ -452,7 +457,8 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   hipError_t e = hrt::launch_trace(p, variant, ctx->stream, &ctx->last_kernel, &ctx->last_block);
   // the persistent kernels recorded this trace's tile costs: the next one can follow a plan
   ctx->plan_valid = e == hipSuccess && (ctx->last_kernel == HRT_KERNEL_BUNDLE_CULL_LDS ||
-                                        ctx->last_kernel == HRT_KERNEL_BUNDLE_BVH_LDS);
+                                        ctx->last_kernel == HRT_KERNEL_BUNDLE_BVH_LDS ||
+                                        ctx->last_kernel == HRT_KERNEL_BUNDLE_WQ);
   if (e != hipSuccess) {
     ctx->event_pool.push_back(ev);
     return hip_fail(ctx, e, "trace kernel launch");
@@ -696,8 +702,8 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   switch (key) {
     case HRT_OPT_KERNEL_VARIANT:
-      if (value < HRT_KERNEL_AUTO || value > HRT_KERNEL_BUNDLE_BVH_LDS)
-        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be an hrt_kernel value (0..8)");
+      if (value < HRT_KERNEL_AUTO || value > HRT_KERNEL_BUNDLE_WQ)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "kernel variant must be an hrt_kernel value (0..9)");
       ctx->variant = (int)value;
       return HRT_OK;
     case HRT_OPT_COUNTERS:
@@ -710,8 +716,8 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       ctx->sec_batch = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_SPLIT:
-      if (value != 1 && value != 2 && value != 4 && value != 8)
-        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "split must be 1, 2, 4 or 8");
+      if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "split must be 0 (auto), 1, 2, 4 or 8");
       ctx->split_k = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_SPLIT_FACTOR:
@@ -722,6 +728,11 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
     case HRT_OPT_PRIORITY:
       if (value < 0 || value > 2) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "priority must be 0, 1 or 2");
       ctx->split_prio = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_WQ_NODE_CAP:
+      if (value != 0 && (value < 128 || value > (1 << 20)))
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "wq node cap must be 0 (auto) or in [128, 2^20]");
+      ctx->wq_node_cap = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_COOP:
       if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "coop must be 0 or 1");

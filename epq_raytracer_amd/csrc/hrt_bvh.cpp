@@ -203,6 +203,8 @@ struct Builder {
     } else {
       r[14] = bits_f(0u);
       build(b, mid - b, tris);
+      // inner node: the right child's index (count bits 27..31 stay 0); the left child is node + 1
+      out.nodes[(size_t)node * 16 + 14] = bits_f(out.n_nodes);
       build(mid, b + n - mid, tris);
     }
     out.nodes[(size_t)node * 16 + 15] = bits_f(out.n_nodes);  // escape: first node after the subtree

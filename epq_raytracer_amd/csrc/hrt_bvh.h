@@ -24,7 +24,7 @@ namespace hrt {
 //   [11]    cos(phi)   (phi >= angle(c, n_i / |n_i|) for every triangle; (0, 1) = no cone)
 //   [12]    sin(phi)
 //   [13]    rho = max |n_i - e1_i x e2_i| / |n_i|   (record normal vs exact cross product)
-//   [14]    bits: leaf ? first_prim | count << 27 : 0
+//   [14]    bits: leaf ? first_prim | count << 27 : right child (the left child is the next node)
 //   [15]    bits: escape node (preorder successor that is not a descendant; n_nodes = end)
 // 16 floats per prim: (a, key bits) (e1, mesh bits) (e2, triangle index bits) (n, 0).
 //

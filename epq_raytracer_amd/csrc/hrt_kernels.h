@@ -54,6 +54,8 @@ struct TraceParams {
   const uint32_t* bvh_keybase;   // per mesh: key = keybase[m] + triangle index
   uint32_t bvh_n_nodes, bvh_n_irregular, bvh_n_prims, bvh_n_meshes;
   float bvh_abs_coef, bvh_rel_t;  // box-test t-slack (hrt_bvh.h)
+  uint32_t bvh_max_leaf;         // largest leaf triangle count of the hierarchy
+  uint32_t wq_ncap, wq_tcap;     // BUNDLE_WQ: per-wave node / triangle pair stack capacities (launch_trace)
 };
 
 // Launches the trace kernel(s); *ran / *block receive the resolved hrt_kernel and workgroup size.

@@ -1104,12 +1104,296 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
   }
 }
 
+// ---- BUNDLE_WQ: pair-queue hierarchy traversal for bounce segments --------------------------------
+// The per-lane traversal above (BUNDLE_BVH) keeps one node cursor per lane: a wave runs as many
+// trips as its longest lane (123 per batch vs 55 visits per lane on island) and a leaf's triangles
+// serially, and a heavy 8x8 tile spends ~600K clocks per bounce batch either way (profiles/
+// r01k_tile_profiles.jsonl, BUNDLE_CULL_LDS: ~850 survivor triangles x every lane).  Here the work of
+// a bounce batch is a set of (ray, inner node) and (ray, triangle) PAIRS held in two per-wave LIFO
+// stacks in LDS; every step hands 64 pairs of one kind to the 64 lanes, so lanes stay full whatever the
+// rays' directions.  A node pair tests both children of its node for its ray, pushes the inner ones
+// (the farther first, and all of a step's nearer children above all its farther ones, so the next
+// step descends toward the rays' nearest hits) and the leaves' triangles.  The ray of a pair is read
+// from its owner lane (ds_bpermute); its closest hit so far is a 64-bit LDS slot (t bits << 32 |
+// (mesh << 26 | triangle) + 1), lowered with ds_min_u64: the minimum over every triangle the
+// reference accepts of (dist, scan position), i.e. raytracing.glsl's strict '<' in scan order (spheres
+// hold key 0 and win ties, as they are scanned first).  A child is dropped only by BUNDLE_BVH's exact
+// node test (wq_node_visit) against the slot's current t, which only ever exceeds the final one.
+// When the node stack could overflow, the popped pairs' subtrees are walked stacklessly instead.
+struct WqLds {
+  const float4* nodes;        // BVH nodes (LDS copy)
+  unsigned long long* slot;   // 64 per wave: closest hit so far per ray (owner lane)
+  uint32_t* ns;               // node-pair stack: inner node << 6 | ray
+  uint32_t* ts;               // triangle-pair stack: leaf prim << 6 | ray
+  uint32_t ncap;              // node stack capacity (>= 256)
+};
+
+__device__ __forceinline__ f3 shfl3(f3 v, uint32_t r) {
+  return mk(__shfl(v.x, (int)r, 64), __shfl(v.y, (int)r, 64), __shfl(v.z, (int)r, 64));
+}
+
+// bvh_node_visit with the hardware square root (1 ulp; the extra 2e-7 keeps the cone's sine an upper
+// bound, so a node is only ever kept more often) and the box entry distance for ordering.
+__device__ __forceinline__ bool wq_node_visit(const float4* nd, f3 o, f3 d, f3 inv, float R, float abs_t, float t_hi,
+                                              float& t_near) {
+  const float4 N0 = nd[0], N1 = nd[1], N2 = nd[2], N3 = nd[3];
+  const float x = N2.x * d.x + N2.y * d.y + N2.z * d.z;
+  const float xa = fmaxf(fabsf(x) - 2e-6f, 0.0f);
+  const float s_up = __builtin_amdgcn_sqrtf(fmaxf(1.0f - xa * xa, 0.0f)) + 1.2e-6f;
+  if (x * N2.w - s_up * N3.x - 1e-6f > 1e-5f) return false;  // back: every dn > 0
+  const float mg = N0.w + N1.w * R;
+  const float tx0 = ((N0.x - mg) - o.x) * inv.x, tx1 = ((N1.x + mg) - o.x) * inv.x;
+  const float ty0 = ((N0.y - mg) - o.y) * inv.y, ty1 = ((N1.y + mg) - o.y) * inv.y;
+  const float tz0 = ((N0.z - mg) - o.z) * inv.z, tz1 = ((N1.z + mg) - o.z) * inv.z;
+  const float tn = fmaxf(fmaxf(-abs_t, fminf(tx0, tx1)), fmaxf(fminf(ty0, ty1), fminf(tz0, tz1)));
+  const float tf = fminf(fminf(t_hi, fmaxf(tx0, tx1)), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
+  t_near = tn;
+  return !((tn - fabsf(tn) * 1e-6f) > (tf + fabsf(tf) * 1e-6f));  // NaN -> visit
+}
+
+// Exact reference test (raytracing.glsl:213-241) of BVH leaf prim record (a, -) (e1, -) (e2, -) (n, -):
+// true with dist when the reference accepts the triangle (dist > 0.001, u, v, w >= 0); the division-free
+// pre-test (pre_reject) skips candidates beyond best_k first.
+__device__ __forceinline__ bool wq_tri_accept(const float4& A, const float4& B, const float4& C, const float4& N, f3 o,
+                                              f3 d, float best_k, float& dist) {
+  const f3 n = mk(N.x, N.y, N.z);
+  const f3 ao = o - mk(A.x, A.y, A.z);
+  TriPre q;
+  q.num_t = dot(ao, n);
+  if (!(q.num_t > 0.0f)) return false;
+  const float dn = dot(d, n);
+  if (!(dn < 0.0f)) return false;
+  const f3 dao = cross(ao, d);
+  q.num_u = dot(mk(C.x, C.y, C.z), dao);
+  q.num_v = dot(mk(B.x, B.y, B.z), dao);
+  q.det = -dn;
+  if (pre_reject(q, best_k)) return false;
+  const float inv_det = 1.0f / q.det;
+  dist = q.num_t * inv_det;
+  const float u = q.num_u * inv_det;
+  const float v = -q.num_v * inv_det;
+  const float w = 1.0f - u - v;
+  return !(dist < 0.0f) && !(u < 0.0f) && !(v < 0.0f) && !(w < 0.0f) && dist > 0.001f;
+}
+
+__device__ __forceinline__ float wq_slot_t(const WqLds& wq, uint32_t r) {
+  return __uint_as_float(reinterpret_cast<const uint32_t*>(wq.slot)[2 * r + 1]);
+}
+
+// Leaf prim k for ray r (origin o, direction d, mesh filter mask): test and lower the ray's slot.
+__device__ __forceinline__ void wq_leaf_prim(const TraceParams& P, const WqLds& wq, uint32_t k, uint32_t r,
+                                             unsigned long long mask, f3 o, f3 d) {
+  const float4* pr = P.bvh_prims;
+  const float4 A = pr[4 * k], B = pr[4 * k + 1], C = pr[4 * k + 2], N = pr[4 * k + 3];
+  const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
+  if (!((mask >> m) & 1ull)) return;  // mesh failed its (quirky) AABB test for this ray
+  float dist;
+  if (wq_tri_accept(A, B, C, N, o, d, wq_slot_t(wq, r) * kOnePlus, dist)) {
+    const uint32_t id = ((m << 26) | __builtin_bit_cast(uint32_t, C.w)) + 1u;
+    atomicMin(&wq.slot[r], ((unsigned long long)__float_as_uint(dist) << 32) | id);
+  }
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+
+template <bool D>
+__device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const TraceParams& P, const WqLds& wq, bool sec,
+                                                    f3 o, f3 d, uint32_t& tests, Closest& c, Diag& dg) {
+  const hrt_push_constants& pc = P.pc;
+  const uint32_t lane = threadIdx.x & 63;
+  spheres_first(sc, pc, sec, o, d, c);
+  unsigned long long mask = 0ull;
+  if (sec) {
+    for (int m = 0; m < pc.num_meshes; ++m) {
+      const hrt_mesh& mesh = sc.meshes[m];
+      if (aabb_pass(mesh, o, d)) {
+        mask |= 1ull << m;
+        tests += mesh.len;
+      }
+    }
+  }
+  // the irregular list and this lane's grazing-band list: per lane, as in BUNDLE_BVH
+  uint32_t bkey = 0;
+  float best_k = c.t * kOnePlus;
+  const BvhGlobal g{P.bvh_nodes, P.bvh_prims};
+  for (uint32_t k = 0; k < P.bvh_n_irregular; ++k)
+    if (sec) bvh_prim_test(P.bvh_irregular, k, mask, o, d, c, bkey, best_k);
+  const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  float R;
+  {  // farthest root-box corner from the origin, rounded up
+    const float4 R0 = wq.nodes[0], R1 = wq.nodes[1];
+    const float fx = fmaxf(fabsf(o.x - R0.x), fabsf(R1.x - o.x)), fy = fmaxf(fabsf(o.y - R0.y), fabsf(R1.y - o.y));
+    const float fz = fmaxf(fabsf(o.z - R0.z), fabsf(R1.z - o.z));
+    R = __builtin_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0001f;
+  }
+  const float abs_t = P.bvh_abs_coef * R;
+  uint32_t band_tests = 0;
+#ifdef HRT_WQ_NOBAND
+  if (false) {
+#else
+  if (sec && mask) {
+#endif
+    const uint32_t cell = dir_cell(d);
+    const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
+    const float lo = -kBandTau - 2e-5f, hi = 3e-5f;  // see world_hit_bounce_bvh
+    uint32_t k = b0;
+    for (; k + 4 <= b1; k += 4) {
+      const float4 qs[4] = {P.bvh_band[k], P.bvh_band[k + 1], P.bvh_band[k + 2], P.bvh_band[k + 3]};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float dn = d.x * qs[j].x + d.y * qs[j].y + d.z * qs[j].z;
+        if (dn > lo && dn < hi) {
+          g.prim(__builtin_bit_cast(uint32_t, qs[j].w), mask, o, d, c, bkey, best_k);
+          ++band_tests;
+        }
+      }
+    }
+    for (; k < b1; ++k) {
+      const float4 q = P.bvh_band[k];
+      const float dn = d.x * q.x + d.y * q.y + d.z * q.z;
+      if (dn > lo && dn < hi) {
+        g.prim(__builtin_bit_cast(uint32_t, q.w), mask, o, d, c, bkey, best_k);
+        ++band_tests;
+      }
+    }
+  }
+  // pair traversal: the root is tested per lane, then (ray, inner node) / (ray, triangle) pairs
+  const uint32_t id0 = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
+  wq.slot[lane] = ((unsigned long long)__float_as_uint(c.t) << 32) | id0;
+  uint32_t rinfo = 0;
+  bool rvis = false;
+  if (sec && mask) {
+    float tn;
+    rinfo = __builtin_bit_cast(uint32_t, wq.nodes[3].z);
+    rvis = wq_node_visit(wq.nodes, o, d, inv, R, abs_t, c.t * (1.0f + P.bvh_rel_t) + abs_t, tn);
+  }
+  const uint32_t rcnt = rvis ? rinfo >> 27 : 0u;
+  const unsigned long long rb = __ballot(rvis && rcnt == 0u);
+  if (rvis && rcnt == 0u) wq.ns[lanes_below(rb)] = lane;  // inner root: pair (ray, node 0)
+  uint32_t nc = (uint32_t)__popcll(rb), tc = 0;
+  {  // leaf root (a scene of at most leaf-size triangles): its triangles
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const unsigned long long bb = __ballot((rcnt >> b) & 1u);
+      pre += lanes_below(bb) << b;
+      tot += (uint32_t)__popcll(bb) << b;
+    }
+    for (uint32_t j = 0; j < rcnt; ++j) wq.ts[pre + j] = (((rinfo & 0x07FFFFFFu) + j) << 6) | lane;
+    tc = tot;
+  }
+  uint32_t node_pairs = 0, tri_pairs = 0, steps = 0;
+  while (nc | tc) {
+    ++steps;
+    if (tc >= 64u || nc == 0u) {  // triangle step
+      const uint32_t take = min(64u, tc);
+      tc -= take;
+      tri_pairs += take;
+      const bool act = lane < take;
+      const uint32_t e = act ? wq.ts[tc + lane] : lane;
+      const uint32_t r = e & 63u;
+      const f3 ro = shfl3(o, r), rd = shfl3(d, r);
+      const unsigned long long rm =
+          ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
+          (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
+      if (act) wq_leaf_prim(P, wq, e >> 6, r, rm, ro, rd);
+      continue;
+    }
+    // node step: pair (ray r, inner node p) tests p's children
+    const uint32_t take = min(64u, nc);
+    nc -= take;
+    node_pairs += take;
+    const bool act = lane < take;
+    const uint32_t e = act ? wq.ns[nc + lane] : lane;
+    const uint32_t r = e & 63u, p = e >> 6;
+    const f3 ro = shfl3(o, r), rd = shfl3(d, r), rinv = shfl3(inv, r);
+    const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
+    const unsigned long long rm =
+        ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
+        (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
+    const bool overflow = nc + 2u * take > wq.ncap;  // wave-uniform
+    bool vl = false, vr = false;
+    uint32_t il = 0, ir = 0, cr = 0;
+    float tl = 0.0f, tr = 0.0f;
+    if (act) {
+      const float4 P3 = wq.nodes[4 * p + 3];
+      cr = __builtin_bit_cast(uint32_t, P3.z);  // right child; the left one is p + 1
+      if (!overflow) {
+        const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
+        il = __builtin_bit_cast(uint32_t, wq.nodes[4 * (p + 1) + 3].z);
+        ir = __builtin_bit_cast(uint32_t, wq.nodes[4 * cr + 3].z);
+        vl = wq_node_visit(wq.nodes + 4 * (p + 1), ro, rd, rinv, rR, rabs, t_hi, tl);
+        vr = wq_node_visit(wq.nodes + 4 * cr, ro, rd, rinv, rR, rabs, t_hi, tr);
+      } else {  // finish p's subtree below p with a stackless walk (escape links)
+        const uint32_t end = __builtin_bit_cast(uint32_t, P3.w);
+        uint32_t cur = p + 1;
+        while (cur < end) {
+          const uint32_t inf = __builtin_bit_cast(uint32_t, wq.nodes[4 * cur + 3].z), cnt = inf >> 27;
+          float tn;
+          const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
+          const bool v = wq_node_visit(wq.nodes + 4 * cur, ro, rd, rinv, rR, rabs, t_hi, tn);
+          if (v && cnt) {
+            const uint32_t first = inf & 0x07FFFFFFu;
+            for (uint32_t k = first; k < first + cnt; ++k) wq_leaf_prim(P, wq, k, r, rm, ro, rd);
+          }
+          cur = (v && !cnt) ? cur + 1 : __builtin_bit_cast(uint32_t, wq.nodes[4 * cur + 3].w);
+        }
+      }
+    }
+    const uint32_t cl = vl ? il >> 27 : 0u, cnr = vr ? ir >> 27 : 0u;  // leaf triangle counts
+    const bool inl = vl && cl == 0u, inr = vr && cnr == 0u;             // inner children kept
+    // inner children: every lane's farther (or only) child below every lane's nearer one
+    const bool both = inl && inr;
+    const bool l_near = tl <= tr;
+    const uint32_t far_node = both ? (l_near ? cr : p + 1u) : (inl ? p + 1u : cr);
+    const uint32_t near_node = l_near ? p + 1u : cr;
+    const unsigned long long fb = __ballot(inl || inr), bb2 = __ballot(both);
+    const uint32_t nfar = (uint32_t)__popcll(fb);
+    if (inl || inr) wq.ns[nc + lanes_below(fb)] = (far_node << 6) | r;
+    if (both) wq.ns[nc + nfar + lanes_below(bb2)] = (near_node << 6) | r;
+    nc += nfar + (uint32_t)__popcll(bb2);
+    // leaf children's triangles: exclusive prefix of the per-lane counts (0..32) from bit-plane ballots
+    const uint32_t cnt = cl + cnr;
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const unsigned long long bb = __ballot((cnt >> b) & 1u);
+      pre += lanes_below(bb) << b;
+      tot += (uint32_t)__popcll(bb) << b;
+    }
+    if (cl) {
+      const uint32_t first = il & 0x07FFFFFFu;
+      for (uint32_t j = 0; j < cl; ++j) wq.ts[tc + pre + j] = ((first + j) << 6) | r;
+    }
+    if (cnr) {
+      const uint32_t first = ir & 0x07FFFFFFu;
+      for (uint32_t j = 0; j < cnr; ++j) wq.ts[tc + pre + cl + j] = ((first + j) << 6) | r;
+    }
+    tc += tot;
+  }
+  if (sec) {
+    const unsigned long long s = wq.slot[lane];
+    const uint32_t id = (uint32_t)s;
+    if (id != 0u) c = Closest{__uint_as_float((uint32_t)(s >> 32)), 2, (id - 1u) & 0x03FFFFFFu, (id - 1u) >> 26};
+  }
+  if (D && P.diag) {  // wave totals, held by lane 0 (the tile record sums lanes)
+    if (lane == 0) {
+      dg.bvh_visits += node_pairs;
+      dg.bvh_prims += tri_pairs;
+      dg.bvh_trips += steps;
+    }
+    dg.bvh_band += band_tests;
+  }
+}
+
 // Fused loop of BUNDLE / BUNDLE_CULL / BUNDLE_BVH.  Every lane stays in the loop until the whole wave is done, so
 // the loop top is a full-wave region (lane-parallel culls and shuffles need all 64 lanes).  Primary
 // segments take the bundle path; a lane whose next segment is a bounce waits (state untouched) until
 // at least sec_batch lanes wait or no primary segment is left in the wave, then all waiting lanes run
 // their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
-enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2 };
+enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2, kBounceWq = 3 };
 
 template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, const CullSrc& csrc,
@@ -1174,7 +1458,9 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     }
     if (D && P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
-      if constexpr (Bounce == kBounceBvh) {
+      if constexpr (Bounce == kBounceWq) {
+        world_hit_bounce_wq<D>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
+      } else if constexpr (Bounce == kBounceBvh) {
         world_hit_bounce_bvh<D>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
       } else if constexpr (Bounce == kBounceCull) {
         world_hit_bounce_cull<D>(sc, P, csrc, sec, p.pos, p.dir, tests, c, dg, co);
@@ -1210,8 +1496,14 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     unsigned long long* rec = P.tile_cycles + 4 * ((lr / 8) * tiles_x + x / 8);
     atomicMax(&rec[0], (unsigned long long)(__builtin_readcyclecounter() - tile_t0));  // slowest item of a split tile
     atomicAdd(&rec[1], (unsigned long long)dg.sec_iters);
-    atomicAdd(&rec[2], (unsigned long long)dg.sec_survivors);
+    if (Bounce != kBounceBvh && Bounce != kBounceWq) atomicAdd(&rec[2], (unsigned long long)dg.sec_survivors);
     atomicAdd(&rec[3], (unsigned long long)dg.cyc_sec);
+  }
+  if (D && P.tile_cycles && (Bounce == kBounceBvh || Bounce == kBounceWq) && active) {
+    // BUNDLE_BVH: the tile's per-lane node visits, summed | (leaf + band triangle tests) << 32
+    const uint32_t tiles_x = (pc.width + 7) / 8;
+    atomicAdd(P.tile_cycles + 4 * ((lr / 8) * tiles_x + x / 8) + 2,
+              (unsigned long long)dg.bvh_visits + ((unsigned long long)(dg.bvh_prims + dg.bvh_band) << 32));
   }
   if (P.diag && (threadIdx.x & 63) == 0) {
     atomicAdd(&P.diag[10], (unsigned long long)dg.cyc_prim);
@@ -1229,7 +1521,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[5], (unsigned long long)dg.sec_survivors);
     atomicAdd(&P.diag[6], (unsigned long long)dg.sec_lanes);
   }
-  if (P.diag && Bounce == kBounceBvh) {
+  if (P.diag && (Bounce == kBounceBvh || Bounce == kBounceWq)) {
     atomicAdd(&P.diag[7], (unsigned long long)dg.bvh_visits);
     atomicAdd(&P.diag[8], (unsigned long long)dg.bvh_prims);
     atomicAdd(&P.diag[9], (unsigned long long)dg.bvh_band);
@@ -1467,6 +1759,23 @@ __global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
   });
 }
 
+// BUNDLE_WQ: the hierarchy's nodes in LDS, one pair-stack region per wave after them (persistent
+// 1024-thread workgroups).  Dynamic LDS: [nodes x 64 B][16 x (64 slots x 8 B, wq_ncap + wq_tcap words)].
+template <bool D>
+__global__ __launch_bounds__(1024) void trace_bundle_wq(TraceParams P) {
+  const uint32_t nn = P.bvh_n_nodes;
+  float4* nodes = lds_tris;
+  for (uint32_t k = threadIdx.x; k < 4 * nn; k += 1024) nodes[k] = P.bvh_nodes[k];
+  char* base = reinterpret_cast<char*>(nodes + 4 * nn) + (size_t)(threadIdx.x >> 6) * (512 + 4 * (P.wq_ncap + P.wq_tcap));
+  const WqLds wq{nodes, reinterpret_cast<unsigned long long*>(base), reinterpret_cast<uint32_t*>(base + 512),
+                 reinterpret_cast<uint32_t*>(base + 512) + P.wq_ncap, P.wq_ncap};
+  __syncthreads();
+  const float4* T = reinterpret_cast<const float4*>(P.tris);
+  tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co) {
+    trace_fused_split<kBounceWq, D>(P, x, lr, CullGlobal{T, to_const(T)}, wq, nullptr, co);
+  });
+}
+
 // BUNDLE_BVH with the hierarchy and the triangle image in LDS (persistent 1024-thread workgroups).
 // Dynamic LDS: [n_tris x 48 B triangles][nodes x 64 B][prims x 4 B entries][meshes x 4 B key bases].
 template <bool D>
@@ -1640,22 +1949,44 @@ uint32_t lds_block(uint32_t n) {
   return tri <= kMaxLdsScene / 2 ? 512u : tri <= kMaxLdsScene ? 1024u : 0u;
 }
 
+// BUNDLE_WQ per-wave pair stacks: triangle stack 64 x (1 + 2 x largest leaf), node stack what is left of
+// the 160 KiB after the nodes (at most 1024 pairs, at least 128).  Returns the LDS bytes, 0 = no fit.
+size_t wq_lds_bytes(const TraceParams& p, uint32_t* ncap, uint32_t* tcap) {
+  if (!p.bvh_nodes || p.bvh_max_leaf > 4) return 0;
+  const size_t nodes = (size_t)p.bvh_n_nodes * 64, t = 64u * (1u + 2u * p.bvh_max_leaf);
+  if (nodes + 16 * (512 + 4 * (t + 128)) > kMaxLdsScene) return 0;
+  const size_t per_wave = (kMaxLdsScene - nodes) / 16;
+  const uint32_t n = (uint32_t)std::min<size_t>(1024, ((per_wave - 512 - 4 * t) / 4) & ~(size_t)63);
+  if (ncap) *ncap = n;
+  if (tcap) *tcap = (uint32_t)t;
+  return nodes + 16 * (512 + 4 * ((size_t)n + t));
+}
+
 int resolve_variant(const TraceParams& p, int variant) {
   if (variant == HRT_KERNEL_AUTO) {
-    // profiles/r01g_*: island 21.4 (LDS) vs 23.7 ms, cave 112 vs 120 ms; BVH from ~4K triangles
-    variant = p.cam_list_capacity >= kAutoBvhTris && p.bvh_nodes ? HRT_KERNEL_BUNDLE_BVH
-              : p.cam_list_capacity < kAutoCullTris              ? HRT_KERNEL_BUNDLE
+    // profiles/r01g_*: island 21.4 (LDS) vs 23.7 ms, cave 112 vs 120 ms; BVH from ~4K triangles.
+    // BUNDLE_WQ when its node stacks get >= 512 pairs (profiles/r01m_*: island 8.1 vs 15.6 ms; with
+    // 192 (cave) the stackless fallback runs too often: 60-78 vs 31 ms)
+    uint32_t ncap = 0;
+    const bool wq = wq_lds_bytes(p, &ncap, nullptr) && ncap >= 512 && p.pc.num_meshes <= 64;
+    variant = p.cam_list_capacity < kAutoCullTris                   ? HRT_KERNEL_BUNDLE
+              : wq                                                 ? HRT_KERNEL_BUNDLE_WQ
+              : p.cam_list_capacity >= kAutoBvhTris && p.bvh_nodes ? HRT_KERNEL_BUNDLE_BVH
               : lds_block(p.n_tris) != 0                ? HRT_KERNEL_BUNDLE_CULL_LDS
                                                                  : HRT_KERNEL_BUNDLE_CULL;
   }
   if (variant == HRT_KERNEL_BRUTE_LDS && (size_t)p.n_tris * 48 > kMaxLdsScene) variant = HRT_KERNEL_BRUTE;
   if (variant == HRT_KERNEL_BUNDLE_BVH && (!p.bvh_nodes || p.pc.num_meshes > 64)) variant = HRT_KERNEL_BUNDLE_CULL;
   if (variant == HRT_KERNEL_BUNDLE_CULL_LDS && lds_block(p.n_tris) == 0) variant = HRT_KERNEL_BUNDLE_CULL;
+  if (variant == HRT_KERNEL_BUNDLE_WQ && (wq_lds_bytes(p, nullptr, nullptr) == 0 || p.pc.num_meshes > 64))
+    variant = HRT_KERNEL_BUNDLE_BVH_LDS;
   if (variant == HRT_KERNEL_BUNDLE_BVH_LDS && !bvh_lds_fits(p)) variant = HRT_KERNEL_BUNDLE_BVH;
   if (variant == HRT_KERNEL_BUNDLE_BVH_LDS && (!p.bvh_nodes || p.pc.num_meshes > 64)) variant = HRT_KERNEL_BUNDLE_CULL;
   if (p.pc.max_bounces < 0) variant = HRT_KERNEL_LITERAL;  // the fused loops assume >= 1 segment per path
   return variant;
 }
+
+static uint32_t tiles_of(const TraceParams& p) { return ((p.pc.width + 7) / 8) * ((p.local_rows + 7) / 8); }
 
 // Persistent kernels: plan this trace from the last one's tile costs (when p.plan_valid and
 // splitting is on), then reset the counters the trace fills.  q.items = nullptr: plain tile order.
@@ -1690,7 +2021,9 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
     const void* whole_cu[] = {reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024, false>),
                               reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024, true>),
                               reinterpret_cast<const void*>(&trace_bundle_bvh_lds<false>),
-                              reinterpret_cast<const void*>(&trace_bundle_bvh_lds<true>)};
+                              reinterpret_cast<const void*>(&trace_bundle_bvh_lds<true>),
+                              reinterpret_cast<const void*>(&trace_bundle_wq<false>),
+                              reinterpret_cast<const void*>(&trace_bundle_wq<true>)};
     for (const void* f : half_cu)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kMaxLdsScene / 2));
     for (const void* f : whole_cu)
@@ -1714,6 +2047,7 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       TraceParams q = p;
       q.coop = 0;
+      if (q.split_k == 0) q.split_k = 1;
       const size_t lds = bvh_lds_bytes(p);
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
       if (p.diag)
@@ -1723,13 +2057,32 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       *block_out = 1024;
       break;
     }
+    case HRT_KERNEL_BUNDLE_WQ: {
+      if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      TraceParams q = p;
+      q.coop = 0;
+      // split auto: a pair step's work scales with the rays in the batch, so a heavy tile's sample
+      // chains run as 4 items of 2 rows (8 of 1 row when a resident wave gets <= 4 tiles: row
+      // partitions at N > 1), profiles/r01m_wq_split.jsonl
+      if (q.split_k == 0) q.split_k = tiles_of(p) > 4 * p.num_cus * 16u ? 4u : 8u;
+      const size_t lds = wq_lds_bytes(p, &q.wq_ncap, &q.wq_tcap);
+      if (p.wq_ncap) q.wq_ncap = std::min(q.wq_ncap, std::max(128u, p.wq_ncap & ~63u));  // HRT_OPT_WQ_NODE_CAP
+      if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
+      if (p.diag)
+        trace_bundle_wq<true><<<p.num_cus, 1024, lds, stream>>>(q);
+      else
+        trace_bundle_wq<false><<<p.num_cus, 1024, lds, stream>>>(q);
+      *block_out = 1024;
+      break;
+    }
     case HRT_KERNEL_BUNDLE_CULL_LDS: {
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       TraceParams q = p;
       const uint32_t block = lds_block(p.n_tris);
       *block_out = (int)block;
       const size_t lds = (size_t)p.n_tris * 48 + kCoopLds;
-      q.coop = p.coop && p.split_k == 1 && p.pc.num_meshes <= 62 ? 1u : 0u;
+      if (q.split_k == 0) q.split_k = 1;  // auto: cooperative heavy tiles instead
+      q.coop = p.coop && q.split_k == 1 && p.pc.num_meshes <= 62 ? 1u : 0u;
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
       if (block == 512) {
         if (p.diag)

@@ -152,8 +152,9 @@ typedef struct hrt_context hrt_context;
 /* Trace kernel variants (HRT_OPT_KERNEL_VARIANT).  All produce byte-identical frames and counters;
  * they differ only in how much of the reference's brute-force work they prove unnecessary. */
 typedef enum hrt_kernel {
-  HRT_KERNEL_AUTO = 0,        /* BUNDLE below 256 mesh triangles; then BUNDLE_CULL_LDS while the triangle
-                                 buffer fits LDS (else BUNDLE_CULL) below 4096; BUNDLE_BVH above */
+  HRT_KERNEL_AUTO = 0,        /* BUNDLE below 256 mesh triangles; then BUNDLE_WQ while the hierarchy fits
+                                 LDS; else BUNDLE_CULL_LDS while the triangle buffer fits LDS (else
+                                 BUNDLE_CULL) below 4096; BUNDLE_BVH above */
   HRT_KERNEL_LITERAL = 1,     /* raytracing.glsl's loop shape, the full test on every triangle */
   HRT_KERNEL_BRUTE = 2,       /* fused sample/bounce loop, two-stage exact pre-test, triangles via SGPRs */
   HRT_KERNEL_BRUTE_LDS = 3,   /* BRUTE with the scene resident in LDS (falls back to BRUTE above 160 KiB) */
@@ -164,8 +165,12 @@ typedef enum hrt_kernel {
                                  mesh triangles) */
   HRT_KERNEL_BUNDLE_CULL_LDS = 7, /* BUNDLE_CULL with the triangle buffer resident in LDS (512/1024-thread
                                     workgroups; falls back to BUNDLE_CULL above ~3,300 triangles) */
-  HRT_KERNEL_BUNDLE_BVH_LDS = 8   /* BUNDLE_BVH with the hierarchy and triangles in LDS (1024-thread
+  HRT_KERNEL_BUNDLE_BVH_LDS = 8,  /* BUNDLE_BVH with the hierarchy and triangles in LDS (1024-thread
                                     workgroups; falls back to BUNDLE_BVH when they exceed 160 KiB) */
+  HRT_KERNEL_BUNDLE_WQ = 9        /* bounce segments through the hierarchy as (ray, node) / (ray, triangle)
+                                    pairs on per-wave LDS stacks, 64 pairs per step (1024-thread
+                                    persistent workgroups, nodes in LDS; falls back to BUNDLE_BVH_LDS when
+                                    they do not fit or leaves exceed 4 triangles) */
 } hrt_kernel;
 
 /* Option keys for hrt_set_option. */
@@ -180,9 +185,10 @@ typedef enum hrt_option {
   HRT_OPT_SECONDARY_BATCH = 3,
   /* BUNDLE_BVH: triangles per leaf of the hierarchy the next hrt_set_scene builds (1..16, default 4) */
   HRT_OPT_BVH_LEAF_SIZE = 4,
-  /* persistent (*_LDS) kernels: a tile that took more than 4x the mean in the previous trace runs as
-   * this many work items of 8/k rows each, scheduled first (1 = off; 2, 4 default, 8).  The frame's
-   * time is set by its slowest tiles' sample chains; results do not depend on it. */
+  /* persistent kernels: a heavy tile (HRT_OPT_SPLIT_FACTOR) of the previous trace runs as this many
+   * work items of 8/k rows each, scheduled first (1 = off, 2, 4, 8; default 0 = auto: BUNDLE_WQ 4, or
+   * 8 when a resident wave gets at most 4 tiles; the others 1).  The frame's time is set by its
+   * slowest tiles' sample chains; results do not depend on it. */
   HRT_OPT_SPLIT = 5,
   /* heavy tile: its cost in the previous trace exceeds this multiple of a resident wave's fair share
    * (sum of tile costs / resident waves), to a half octave (0: every tile is heavy; default -1 =
@@ -195,7 +201,11 @@ typedef enum hrt_option {
   HRT_OPT_GRID_CUS = 8,
   /* BUNDLE_CULL_LDS with HRT_OPT_SPLIT = 1: heavy tiles run cooperatively, every wave of a workgroup
    * on the same tile with the bounce cull's chunks dealt out over the waves (1 default, 0 off) */
-  HRT_OPT_COOP = 9
+  HRT_OPT_COOP = 9,
+  /* BUNDLE_WQ: per-wave node-pair stack capacity (0 = what fits the LDS, default; else at most that,
+   * rounded down to a multiple of 64, >= 128).  A step that could overflow it walks its pairs'
+   * subtrees stacklessly instead; results do not depend on it (tests force the fallback with 128). */
+  HRT_OPT_WQ_NODE_CAP = 10
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */

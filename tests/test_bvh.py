@@ -151,6 +151,7 @@ def test_tree_structure_boxes_and_cones(built):
         else:
             left_end = walk(k + 1)
             assert int(Nu[k + 1, 15]) == left_end
+            assert first == left_end  # inner node word 14: the right child
             for c in (k + 1, left_end):  # children nest in the parent box
                 assert (N[c, 0:3] >= lo).all() and (N[c, 4:7] <= hi).all()
             end = walk(left_end)

@@ -14,7 +14,7 @@ from helpers import E, SceneCase, _lib, mismatch_report
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [0, 1]  # auto (tuned), literal
-ALL_VARIANTS = list(range(9))  # every hrt_kernel value (hrt_set_option HRT_OPT_KERNEL_VARIANT)
+ALL_VARIANTS = list(range(10))  # every hrt_kernel value (hrt_set_option HRT_OPT_KERNEL_VARIANT)
 
 CONFIGS = [
     # (scene, size, spp, bounces, rng_offset)
@@ -56,7 +56,8 @@ def test_every_variant_bit_exact(scene, size, spp, bounces, variant):
 @pytest.mark.parametrize("split,factor,prio", [(1, 4, 0), (1, 4, 1), (1, 0, 1), (2, 0, 0), (4, 0, 1), (8, 0, 0),
                                                (4, 4, 1), (8, 2, 1)])
 @pytest.mark.parametrize("scene,size,spp,bounces,variant", [("cave", (64, 48), 2, 8, 7), ("island", (75, 41), 3, 8, 7),
-                                                            ("island", (75, 41), 3, 8, 8)])
+                                                            ("island", (75, 41), 3, 8, 8), ("island", (75, 41), 3, 8, 9),
+                                                            ("cave", (64, 48), 2, 8, 9)])
 def test_split_schedule_bit_exact(scene, size, spp, bounces, variant, split, factor, prio):
     """The persistent kernels' second and later traces follow the planner's work items: tiles that
     cost more than factor x the mean last time run first, as `split` row groups, at raised wave
@@ -121,12 +122,40 @@ def test_coop_tiles_bit_exact(scene, factor):
     ctx.close()
 
 
-@pytest.mark.parametrize("split,coop", [(8, 0), (1, 1)])
-def test_split_schedule_partition_and_scene_change(split, coop):
+@pytest.mark.parametrize("cap", [0, 128])
+@pytest.mark.parametrize("split", [0, 1])
+@pytest.mark.parametrize("scene", ["island", "cave", "box", "spheres", "ties"])
+def test_wq_pairs_bit_exact(scene, split, cap):
+    """BUNDLE_WQ: bounce rays through the hierarchy as (ray, node) / (ray, triangle) pairs on per-wave
+    LDS stacks, closest hits merged by (t, scan order) with LDS atomics; cap 128 forces the stackless
+    subtree fallback on most node steps.  Unplanned, then planned (split heavy tiles) traces."""
+    sizes = {"island": (75, 41, 3), "cave": (64, 48, 2), "box": (45, 33, 3), "spheres": (40, 30, 2)}
+    if scene == "ties":
+        case = _tie_soup()
+    else:
+        w, h, spp = sizes[scene]
+        case = SceneCase(scene, (w, h), spp, 8)
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context(variant=9, options={_lib.OPT_SPLIT: split, _lib.OPT_WQ_NODE_CAP: cap,
+                                           _lib.OPT_SPLIT_FACTOR: 0})
+    for _ in range(3):
+        ctx.reset_stats()
+        ctx.trace(case.push())
+        st = ctx.stats()
+        img = ctx.read(_lib.IMG_TRACE)
+        assert np.array_equal(img, ref), mismatch_report(img, ref)
+        assert (st.segments, st.tri_tests) == (seg, tt)
+        if ctx.scene_info()["bvh_built"]:
+            assert st.last_kernel == 9
+    ctx.close()
+
+
+@pytest.mark.parametrize("split,coop,variant", [(8, 0, 7), (1, 1, 7), (0, 0, 9), (8, 0, 9)])
+def test_split_schedule_partition_and_scene_change(split, coop, variant):
     """Ragged row-tile partition (local rows not a multiple of 8) with every tile split (or run
     cooperatively), and a scene switch in between (the old costs are dropped)."""
     case = SceneCase("island", (80, 70), 2, 8)
-    ctx = case.context(partition=(4, 1, 3), variant=7,
+    ctx = case.context(partition=(4, 1, 3), variant=variant,
                        options={_lib.OPT_SPLIT: split, _lib.OPT_SPLIT_FACTOR: 0, _lib.OPT_COOP: coop})
     ctx.trace(case.push())
     first = ctx.read(_lib.IMG_TRACE)
@@ -152,9 +181,13 @@ def test_split_schedule_partition_and_scene_change(split, coop):
 def test_split_options_validated():
     case = SceneCase("box", (16, 16), 1, 1)
     ctx = case.context(variant=7)
-    for bad in (0, 3, 16):
+    for bad in (-1, 3, 16):
         with pytest.raises(Exception):
             ctx.set_option(_lib.OPT_SPLIT, bad)
+    ctx.set_option(_lib.OPT_SPLIT, 0)  # auto
+    for bad in (1, 127):
+        with pytest.raises(Exception):
+            ctx.set_option(_lib.OPT_WQ_NODE_CAP, bad)
     with pytest.raises(Exception):
         ctx.set_option(_lib.OPT_PRIORITY, 3)
     with pytest.raises(Exception):

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--no-ref", action="store_true", help="skip the literal-kernel reference frame")
     ap.add_argument("--diag", action="store_true", help="also print the bundle kernels' cull diagnostics")
     ap.add_argument("--sec-batch", type=int, nargs="+", default=[48], help="HRT_OPT_SECONDARY_BATCH values to sweep")
-    ap.add_argument("--split", type=int, nargs="+", default=[1], help="HRT_OPT_SPLIT values to sweep (LDS variants)")
+    ap.add_argument("--split", type=int, nargs="+", default=[0], help="HRT_OPT_SPLIT values to sweep (LDS variants)")
     ap.add_argument("--prio", type=int, nargs="+", default=[1], help="HRT_OPT_PRIORITY values to sweep")
     ap.add_argument("--factor", type=int, nargs="+", default=[-1], help="HRT_OPT_SPLIT_FACTOR values to sweep")
     ap.add_argument("--coop", type=int, nargs="+", default=[1], help="HRT_OPT_COOP values to sweep")
@@ -76,7 +76,7 @@ def main():
                 same[(v, sb, k)] = None if ref is None else bool(np.array_equal(ctx.read(_lib.IMG_TRACE), ref))
     if a.diag:
         for v in a.variants:
-            if v in (0, 4, 5, 6, 7, 8):
+            if v in (0, 4, 5, 6, 7, 8, 9):
                 ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
                 ctx.set_option(_lib.OPT_COUNTERS, 2)
                 ctx.reset_stats()

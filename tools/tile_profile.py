@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--variant", type=int, default=0)
-    ap.add_argument("--split", type=int, default=1, help="HRT_OPT_SPLIT (heavy tiles as k items)")
+    ap.add_argument("--split", type=int, default=0, help="HRT_OPT_SPLIT (heavy tiles as k items; 0 auto)")
     ap.add_argument("--prio", type=int, default=1, help="HRT_OPT_PRIORITY")
     ap.add_argument("--cus", type=int, default=0, help="HRT_OPT_GRID_CUS (1: tiles run near solo)")
     ap.add_argument("--npz", default=None)
@@ -41,11 +41,15 @@ def main():
     ctx.reset_stats()
     ctx.trace(pc)
     st = ctx.stats()
-    rec = ctx.tile_profile().astype(np.float64)
+    raw = ctx.tile_profile()
+    rec = raw.astype(np.float64)
     ctx.close()
     prof = rec[..., 0]
     flat = prof.ravel()
     its, surv, bcyc = (rec[..., k].ravel() for k in (1, 2, 3))
+    raw2 = raw[..., 2].ravel().astype(np.uint64)
+    bvh = st.last_kernel in (6, 8, 9)  # BUNDLE_BVH*: slot 2 = node visits | (triangle tests << 32), per lane
+    visits, btests = (raw2 & np.uint64(0xFFFFFFFF)).astype(np.float64), (raw2 >> np.uint64(32)).astype(np.float64)
     order = np.argsort(flat)[::-1]
     ty, tx = prof.shape
     res = {"scene": a.scene, "split": a.split, "prio": a.prio, "cus": a.cus, "kernel_ms_diag": st.last_trace_ms, "tiles": int(flat.size),
@@ -54,7 +58,9 @@ def main():
            "max_over_mean": float(flat.max() / flat.mean()),
            "bounce_iters_p50": float(np.median(its)), "bounce_clocks_per_iter_all": float(bcyc.sum() / max(its.sum(), 1)),
            "slowest": [{"tile_x": int(i % tx), "tile_y": int(i // tx), "clocks": float(flat[i]),
-                        "bounce_iters": float(its[i]), "survivors_per_iter": round(surv[i] / max(its[i], 1), 1),
+                        "bounce_iters": float(its[i]),
+                        **({"bvh_visits_per_lane": round(visits[i] / 64, 1), "bvh_tests_per_lane": round(btests[i] / 64, 1)}
+                           if bvh else {"survivors_per_iter": round(surv[i] / max(its[i], 1), 1)}),
                         "bounce_clocks_per_iter": round(bcyc[i] / max(its[i], 1)),
                         "bounce_share": round(bcyc[i] / max(flat[i], 1), 3)} for i in order[:8]]}
     print(json.dumps(res), flush=True)
