@@ -46,7 +46,7 @@ struct BvhHost {
 };
 
 constexpr float kBandTau = 3e-3f;
-constexpr int kDirRes = 64;
+constexpr int kDirRes = 128;
 constexpr int kDirCells = 6 * kDirRes * kDirRes;
 
 constexpr uint32_t kBvhMaxMeshes = 64;     // per-lane mesh filter is a 64-bit mask

@@ -1120,6 +1120,14 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // hold key 0 and win ties, as they are scanned first).  A child is dropped only by BUNDLE_BVH's exact
 // node test (wq_node_visit) against the slot's current t, which only ever exceeds the final one.
 // When the node stack could overflow, the popped pairs' subtrees are walked stacklessly instead.
+#ifndef HRT_WQ_DEEP
+// node steps of at most this many pairs test two levels (lanes would idle).  Off: measured 7.6-7.7 ms
+// without vs 8.2-8.3 ms with 32 on island, no gain on one rank of 8 (profiles/r01n_wq_ab.txt)
+#define HRT_WQ_DEEP 0u
+#endif
+#ifndef HRT_WQ_MIXED
+#define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
+#endif
 struct WqLds {
   const float4* nodes;        // BVH nodes (LDS copy)
   unsigned long long* slot;   // 64 per wave: closest hit so far per ray (owner lane)
@@ -1287,53 +1295,84 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   uint32_t node_pairs = 0, tri_pairs = 0, steps = 0;
   while (nc | tc) {
     ++steps;
-    if (tc >= 64u || nc == 0u) {  // triangle step
-      const uint32_t take = min(64u, tc);
-      tc -= take;
-      tri_pairs += take;
-      const bool act = lane < take;
-      const uint32_t e = act ? wq.ts[tc + lane] : lane;
-      const uint32_t r = e & 63u;
-      const f3 ro = shfl3(o, r), rd = shfl3(d, r);
-      const unsigned long long rm =
-          ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
-          (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
-      if (act) wq_leaf_prim(P, wq, e >> 6, r, rm, ro, rd);
-      continue;
-    }
-    // node step: pair (ray r, inner node p) tests p's children
-    const uint32_t take = min(64u, nc);
-    nc -= take;
-    node_pairs += take;
-    const bool act = lane < take;
-    const uint32_t e = act ? wq.ns[nc + lane] : lane;
-    const uint32_t r = e & 63u, p = e >> 6;
-    const f3 ro = shfl3(o, r), rd = shfl3(d, r), rinv = shfl3(inv, r);
-    const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
+    // Step composition (wave-uniform): triangle pairs when >= 64 wait or no node pair is left; when
+    // both stacks are short, one mixed step takes them all (lanes [0, nn) node pairs, then triangles).
+    const bool tri_step = tc >= 64u || nc == 0u;
+    const bool mixed = HRT_WQ_MIXED && !tri_step && tc > 0u && nc + tc <= 64u;
+    const uint32_t tn = tri_step ? min(64u, tc) : (mixed ? tc : 0u);
+    const uint32_t nn = tri_step ? 0u : min(64u, nc);
+    tc -= tn;
+    nc -= nn;
+    node_pairs += nn;
+    tri_pairs += tn;
+    const bool is_node = lane < nn, is_tri = lane >= nn && lane < nn + tn;
+    const uint32_t e = is_node ? wq.ns[nc + lane] : is_tri ? wq.ts[tc + lane - nn] : lane;
+    const uint32_t r = e & 63u;
+    const f3 ro = shfl3(o, r), rd = shfl3(d, r);
     const unsigned long long rm =
         ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
         (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
-    const bool overflow = nc + 2u * take > wq.ncap;  // wave-uniform
-    bool vl = false, vr = false;
-    uint32_t il = 0, ir = 0, cr = 0;
-    float tl = 0.0f, tr = 0.0f;
-    if (act) {
+    if (is_tri) wq_leaf_prim(P, wq, e >> 6, r, rm, ro, rd);
+    if (nn == 0u) continue;
+    // node pairs (ray r, inner node p): test p's children -- or, when few pairs are left (deep, lanes
+    // idle), skip an inner child's own box and test its two children, two levels per step.  Leaving
+    // a box untested only ever keeps more.  Slots 0..3 hold the nodes tested by this lane.
+    const f3 rinv = shfl3(inv, r);
+    const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
+    const bool deep = nn <= HRT_WQ_DEEP;
+    const bool overflow = nc + (deep ? 4u : 2u) * nn > wq.ncap;  // wave-uniform
+    uint32_t sn[4] = {0u, 0u, 0u, 0u}, si[4] = {0u, 0u, 0u, 0u};
+    bool sk[4] = {false, false, false, false};
+    float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (is_node) {
+      const uint32_t p = e >> 6;
       const float4 P3 = wq.nodes[4 * p + 3];
-      cr = __builtin_bit_cast(uint32_t, P3.z);  // right child; the left one is p + 1
+      const uint32_t cr = __builtin_bit_cast(uint32_t, P3.z);  // right child; the left one is p + 1
       if (!overflow) {
+        bool sv[4] = {true, true, false, false};
+        sn[0] = p + 1u;
+        sn[1] = cr;
+        if (deep) {
+          const uint32_t il = __builtin_bit_cast(uint32_t, wq.nodes[4 * (p + 1) + 3].z);
+          const uint32_t ir = __builtin_bit_cast(uint32_t, wq.nodes[4 * cr + 3].z);
+          sn[2] = cr;
+          sv[2] = true;
+          sv[1] = false;
+          if ((il >> 27) == 0u) {  // inner left child: its children instead
+            sn[0] = p + 2u;
+            sn[1] = il;
+            sv[1] = true;
+          }
+          if ((ir >> 27) == 0u) {
+            sn[2] = cr + 1u;
+            sn[3] = ir;
+            sv[3] = true;
+          }
+        }
         const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
-        il = __builtin_bit_cast(uint32_t, wq.nodes[4 * (p + 1) + 3].z);
-        ir = __builtin_bit_cast(uint32_t, wq.nodes[4 * cr + 3].z);
-        vl = wq_node_visit(wq.nodes + 4 * (p + 1), ro, rd, rinv, rR, rabs, t_hi, tl);
-        vr = wq_node_visit(wq.nodes + 4 * cr, ro, rd, rinv, rR, rabs, t_hi, tr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (sv[k]) {
+            si[k] = __builtin_bit_cast(uint32_t, wq.nodes[4 * sn[k] + 3].z);
+            sk[k] = wq_node_visit(wq.nodes + 4 * sn[k], ro, rd, rinv, rR, rabs, t_hi, st[k]);
+          }
+        }
+        // two children: the nearer one in slot 1, pushed above every lane's slot-0 entries (popped first)
+        if (!deep && st[0] < st[1]) {
+          const uint32_t tnode = sn[0], tinfo = si[0];
+          const bool tk = sk[0];
+          const float tt = st[0];
+          sn[0] = sn[1]; si[0] = si[1]; sk[0] = sk[1]; st[0] = st[1];
+          sn[1] = tnode; si[1] = tinfo; sk[1] = tk; st[1] = tt;
+        }
       } else {  // finish p's subtree below p with a stackless walk (escape links)
         const uint32_t end = __builtin_bit_cast(uint32_t, P3.w);
         uint32_t cur = p + 1;
         while (cur < end) {
           const uint32_t inf = __builtin_bit_cast(uint32_t, wq.nodes[4 * cur + 3].z), cnt = inf >> 27;
-          float tn;
+          float tnear;
           const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
-          const bool v = wq_node_visit(wq.nodes + 4 * cur, ro, rd, rinv, rR, rabs, t_hi, tn);
+          const bool v = wq_node_visit(wq.nodes + 4 * cur, ro, rd, rinv, rR, rabs, t_hi, tnear);
           if (v && cnt) {
             const uint32_t first = inf & 0x07FFFFFFu;
             for (uint32_t k = first; k < first + cnt; ++k) wq_leaf_prim(P, wq, k, r, rm, ro, rd);
@@ -1342,34 +1381,30 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         }
       }
     }
-    const uint32_t cl = vl ? il >> 27 : 0u, cnr = vr ? ir >> 27 : 0u;  // leaf triangle counts
-    const bool inl = vl && cl == 0u, inr = vr && cnr == 0u;             // inner children kept
-    // inner children: every lane's farther (or only) child below every lane's nearer one
-    const bool both = inl && inr;
-    const bool l_near = tl <= tr;
-    const uint32_t far_node = both ? (l_near ? cr : p + 1u) : (inl ? p + 1u : cr);
-    const uint32_t near_node = l_near ? p + 1u : cr;
-    const unsigned long long fb = __ballot(inl || inr), bb2 = __ballot(both);
-    const uint32_t nfar = (uint32_t)__popcll(fb);
-    if (inl || inr) wq.ns[nc + lanes_below(fb)] = (far_node << 6) | r;
-    if (both) wq.ns[nc + nfar + lanes_below(bb2)] = (near_node << 6) | r;
-    nc += nfar + (uint32_t)__popcll(bb2);
-    // leaf children's triangles: exclusive prefix of the per-lane counts (0..32) from bit-plane ballots
-    const uint32_t cnt = cl + cnr;
+    // kept inner nodes: slot-major (every lane's slot 0, then slot 1, ...)
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool inner = sk[k] && (si[k] >> 27) == 0u;
+      const unsigned long long bk = __ballot(inner);
+      if (inner) wq.ns[nc + lanes_below(bk)] = (sn[k] << 6) | r;
+      nc += (uint32_t)__popcll(bk);
+      cnt += sk[k] ? si[k] >> 27 : 0u;  // kept leaves' triangle counts
+    }
+    // kept leaves' triangles: exclusive prefix of the per-lane counts (0..16) from bit-plane ballots
     uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (int b = 0; b < 6; ++b) {
+    for (int b = 0; b < 5; ++b) {
       const unsigned long long bb = __ballot((cnt >> b) & 1u);
       pre += lanes_below(bb) << b;
       tot += (uint32_t)__popcll(bb) << b;
     }
-    if (cl) {
-      const uint32_t first = il & 0x07FFFFFFu;
-      for (uint32_t j = 0; j < cl; ++j) wq.ts[tc + pre + j] = ((first + j) << 6) | r;
-    }
-    if (cnr) {
-      const uint32_t first = ir & 0x07FFFFFFu;
-      for (uint32_t j = 0; j < cnr; ++j) wq.ts[tc + pre + cl + j] = ((first + j) << 6) | r;
+    uint32_t at = tc + pre;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t c = sk[k] ? si[k] >> 27 : 0u, first = si[k] & 0x07FFFFFFu;
+      for (uint32_t j = 0; j < c; ++j) wq.ts[at + j] = ((first + j) << 6) | r;
+      at += c;
     }
     tc += tot;
   }
@@ -1415,6 +1450,9 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   }
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
   const TileList tl = build_tile_list(P, active, centre, list_lds);
+  // bounce batch threshold scaled to the item's active lanes (a split tile's row group has 8/k rows):
+  // a batch of few lanes then runs alongside the other lanes' primary segments instead of after them
+  const uint32_t sec_thresh = max(1u, (P.sec_batch * (uint32_t)__popcll(__ballot(active)) + 63u) / 64u);
   int sample = 0;
   Path p;
   p.bounce = pc.max_bounces + 1;
@@ -1434,7 +1472,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     const bool waiting = !done && p.bounce != 0;
     const uint32_t nwait = (uint32_t)__popcll(__ballot(waiting));
     const bool any_prim = __any(prim);
-    const bool run_sec = nwait > 0 && (nwait >= P.sec_batch || !any_prim);
+    const bool run_sec = nwait > 0 && (nwait >= sec_thresh || !any_prim);
     const bool sec = waiting && run_sec;
     Closest c{kFltMax, 0, 0u, 0u};
     uint64_t t0 = 0, t1 = 0, t2 = 0;
@@ -1495,7 +1533,9 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     const uint32_t tiles_x = (pc.width + 7) / 8;
     unsigned long long* rec = P.tile_cycles + 4 * ((lr / 8) * tiles_x + x / 8);
     atomicMax(&rec[0], (unsigned long long)(__builtin_readcyclecounter() - tile_t0));  // slowest item of a split tile
-    atomicAdd(&rec[1], (unsigned long long)dg.sec_iters);
+    // bounce batches | (BUNDLE_WQ) pair steps << 32
+    atomicAdd(&rec[1], (unsigned long long)dg.sec_iters |
+                           (Bounce == kBounceWq ? (unsigned long long)dg.bvh_trips << 32 : 0ull));
     if (Bounce != kBounceBvh && Bounce != kBounceWq) atomicAdd(&rec[2], (unsigned long long)dg.sec_survivors);
     atomicAdd(&rec[3], (unsigned long long)dg.cyc_sec);
   }
@@ -1585,9 +1625,9 @@ __device__ __forceinline__ void stage_tris(const TraceParams& P, float4* dst, ui
 // is done, so no wave idles while a slower wave of its workgroup finishes.  Every wave leaves the
 // loop once the counter passes the tile count.
 //
-// Work items (P.items, built by plan_fill from the previous trace's per-tile costs): tile | sub << 25.
-// sub == 0 is a whole tile; sub = 1..K covers rows [(sub-1) * 8/K, sub * 8/K) of a heavy tile with
-// 64/K lanes (the rest idle).  A heavy tile's pixels run as K shorter sample chains in parallel
+// Work items (P.items, built by plan_fill from the previous trace's per-tile costs): tile | sub << 25
+// | log2 K << 29 | heavy << 31.  sub == 0 is a whole tile; sub = 1..K covers rows [(sub-1) * 8/K,
+// sub * 8/K) of a heavy tile with 64/K lanes (the rest idle); K grows with the tile's cost.  A heavy tile's pixels run as K shorter sample chains in parallel
 // with lighter batches, and the planner puts them first.  Every pixel is computed exactly once and
 // independently of which wave runs it, so the bytes do not depend on the plan.  Each item's cost goes
 // to P.tile_cost[tile] for the next plan: deterministic work units (Coop::work: survivor tests,
@@ -1649,12 +1689,12 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= n) break;
     const uint32_t item = __builtin_amdgcn_readfirstlane(P.items ? P.items[t] : t);
-    const uint32_t tile = item & 0x01FFFFFFu, sub = (item >> 25) & 15u;
+    const uint32_t tile = item & 0x01FFFFFFu, sub = (item >> 25) & 15u, lk = (item >> 29) & 3u;
     const bool hot = item >> 31;  // heavy last time: issue priority over the light tiles' waves
     const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
     uint32_t x = tx * 8 + (lane & 7), lr = ty * 8 + (lane >> 3);
     if (sub) {
-      const uint32_t rows = 8 / P.split_k, r = lane >> 3;
+      const uint32_t rows = 8u >> lk, r = lane >> 3;
       if (r < rows)
         lr = ty * 8 + (sub - 1) * rows + r;
       else
@@ -1678,9 +1718,9 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
 
 // Planner (after a trace of an LDS variant, before the next).  Items go in decreasing order of the
 // tile's last cost (longest first: a long tile started late is what sets a frame's end), by a
-// 64-bucket half-octave histogram and a descending scan; heavy tiles are the top buckets, k items
-// each: cost >= factor x (sum of costs / resident waves), to the bucket, i.e. a tile that alone
-// would take `factor` times a wave's fair share of the frame.  sched[8..71] histogram, [72..135] bucket offsets,
+// 64-bucket half-octave histogram and a descending scan; heavy tiles are the top buckets: cost >=
+// factor x (sum of costs / resident waves), to the bucket, i.e. a tile that alone would take `factor`
+// times a wave's fair share of the frame; each runs as 2, 4 or 8 items (bucket_items, <= split_k).  sched[8..71] histogram, [72..135] bucket offsets,
 // [136..199] bucket cursors, [3] first heavy bucket.
 constexpr uint32_t kPlanBuckets = 64;
 __device__ __forceinline__ uint32_t cost_bucket(unsigned long long c) {
@@ -1700,23 +1740,30 @@ __global__ __launch_bounds__(256) void plan_hist(uint32_t* sched, const uint32_t
   __syncthreads();
   if (threadIdx.x < kPlanBuckets && h[threadIdx.x]) atomicAdd(&sched[8 + threadIdx.x], h[threadIdx.x]);
 }
-__global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves, uint32_t factor, uint32_t k,
+// Items of a heavy tile in bucket b >= hb: 2 per half-octave pair above the threshold, doubling
+// (costs [1, 2) x threshold: 2 items, [2, 4): 4, then 8), at most kmax; kmax = 1: never split.
+__device__ __forceinline__ uint32_t bucket_items(uint32_t b, uint32_t hb, uint32_t kmax) {
+  return b < hb ? 1u : min(kmax, 2u << min((b - hb) >> 1, 2u));
+}
+__global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves, uint32_t factor, uint32_t kmax,
                                                 uint32_t prio) {
   if (threadIdx.x != 0) return;
   const unsigned long long sum = *reinterpret_cast<const unsigned long long*>(sched + 6);
   const uint32_t hb = cost_bucket((unsigned long long)factor * sum / (waves ? waves : 1u));
-  uint32_t pos = 0, heavy = 0;
+  uint32_t pos = 0, heavy = 0, heavy_items = 0;
   for (int b = (int)kPlanBuckets - 1; b >= 0; --b) {
-    const uint32_t cnt = sched[8 + b], hv = (uint32_t)b >= hb;
+    const uint32_t cnt = sched[8 + b], hv = (uint32_t)b >= hb, k = bucket_items((uint32_t)b, hb, kmax);
     sched[72 + b] = pos;
-    pos += cnt * (hv ? k : 1u);
+    pos += cnt * k;
     heavy += hv ? cnt : 0u;
+    heavy_items += hv ? cnt * k : 0u;
   }
-  sched[1] = prio > 1 ? heavy * k : pos;  // prio 2: heavy items only (diagnostics)
+  sched[1] = prio > 1 ? heavy_items : pos;  // prio 2: heavy items only (diagnostics)
   sched[2] = heavy;
   sched[3] = hb;
 }
-__global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t* cost, uint32_t tiles, uint32_t k,
+// Item word: tile | sub << 25 (1..8, 0 = whole tile) | log2(items of the tile) << 29 | heavy << 31.
+__global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t* cost, uint32_t tiles, uint32_t kmax,
                                                  uint32_t prio, uint32_t* items) {
   __shared__ uint32_t cnt[kPlanBuckets], base[kPlanBuckets];
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -1725,8 +1772,8 @@ __global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t
   const uint32_t hb = sched[3];
   const uint32_t b = i < tiles ? cost_bucket(cost[i]) : 0u;
   const bool heavy = b >= hb;
-  const uint32_t slot = heavy ? k : 1u;
-  const uint32_t local = i < tiles ? atomicAdd(&cnt[b], slot) : 0u;
+  const uint32_t k = bucket_items(b, hb, kmax);
+  const uint32_t local = i < tiles ? atomicAdd(&cnt[b], k) : 0u;
   __syncthreads();
   if (threadIdx.x < kPlanBuckets && cnt[threadIdx.x])
     base[threadIdx.x] = sched[72 + threadIdx.x] + atomicAdd(&sched[136 + threadIdx.x], cnt[threadIdx.x]);
@@ -1737,10 +1784,12 @@ __global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t
     items[at] = i;
   } else {
     const uint32_t flag = prio ? 0x80000000u : 0u;
-    if (k == 1)
+    if (k == 1) {
       items[at] = i | flag;
-    else
-      for (uint32_t s = 0; s < k; ++s) items[at + s] = i | ((s + 1) << 25) | flag;
+    } else {
+      const uint32_t lk = (uint32_t)__builtin_ctz(k);
+      for (uint32_t s = 0; s < k; ++s) items[at + s] = i | ((s + 1) << 25) | (lk << 29) | flag;
+    }
   }
 }
 
@@ -1986,8 +2035,6 @@ int resolve_variant(const TraceParams& p, int variant) {
   return variant;
 }
 
-static uint32_t tiles_of(const TraceParams& p) { return ((p.pc.width + 7) / 8) * ((p.local_rows + 7) / 8); }
-
 // Persistent kernels: plan this trace from the last one's tile costs (when p.plan_valid and
 // splitting is on), then reset the counters the trace fills.  q.items = nullptr: plain tile order.
 static hipError_t prepare_schedule(TraceParams& q, hipStream_t stream) {
@@ -2061,10 +2108,10 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       TraceParams q = p;
       q.coop = 0;
-      // split auto: a pair step's work scales with the rays in the batch, so a heavy tile's sample
-      // chains run as 4 items of 2 rows (8 of 1 row when a resident wave gets <= 4 tiles: row
-      // partitions at N > 1), profiles/r01m_wq_split.jsonl
-      if (q.split_k == 0) q.split_k = tiles_of(p) > 4 * p.num_cus * 16u ? 4u : 8u;
+      // auto: a pair step's work scales with the rays in the batch, so heavy tiles (> 2x a resident
+      // wave's fair share) run as 2, 4 or 8 row groups by cost (profiles/r01n_wq_plan_sweep.jsonl)
+      if (q.split_k == 0) q.split_k = 8;
+      if (q.split_factor < 0) q.split_factor = 2;
       const size_t lds = wq_lds_bytes(p, &q.wq_ncap, &q.wq_tcap);
       if (p.wq_ncap) q.wq_ncap = std::min(q.wq_ncap, std::max(128u, p.wq_ncap & ~63u));  // HRT_OPT_WQ_NODE_CAP
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;

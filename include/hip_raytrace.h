@@ -186,13 +186,13 @@ typedef enum hrt_option {
   /* BUNDLE_BVH: triangles per leaf of the hierarchy the next hrt_set_scene builds (1..16, default 4) */
   HRT_OPT_BVH_LEAF_SIZE = 4,
   /* persistent kernels: a heavy tile (HRT_OPT_SPLIT_FACTOR) of the previous trace runs as this many
-   * work items of 8/k rows each, scheduled first (1 = off, 2, 4, 8; default 0 = auto: BUNDLE_WQ 4, or
-   * 8 when a resident wave gets at most 4 tiles; the others 1).  The frame's time is set by its
-   * slowest tiles' sample chains; results do not depend on it. */
+   * work items of 8/k rows each, scheduled first: at most this many (1 = off, 2, 4, 8; default 0 =
+   * auto: BUNDLE_WQ 8, the others 1), 2 / 4 / 8 as the tile's cost passes 1 / 2 / 4 x the heavy
+   * threshold.  The frame's time is set by its slowest tiles' sample chains; results do not depend on it. */
   HRT_OPT_SPLIT = 5,
   /* heavy tile: its cost in the previous trace exceeds this multiple of a resident wave's fair share
    * (sum of tile costs / resident waves), to a half octave (0: every tile is heavy; default -1 =
-   * auto: 3 when there are more than 4 tiles per resident wave, else 1) */
+   * auto: BUNDLE_WQ 2; the others 3 when there are more than 4 tiles per resident wave, else 1) */
   HRT_OPT_SPLIT_FACTOR = 6,
   /* persistent kernels: heavy tiles (as above) run at raised wave issue priority (1 default, 0 off;
    * 2 = diagnostics: a planned trace runs ONLY the heavy tiles, the frame is incomplete) */

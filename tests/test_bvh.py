@@ -18,7 +18,7 @@ import pytest
 from helpers import E, SceneCase, _lib
 
 TAU_G = np.float32(3e-3)   # hrt_bvh.h kBandTau
-DIR_RES = 64               # hrt_bvh.h kDirRes
+DIR_RES = 128              # hrt_bvh.h kDirRes
 CELLS = 6 * DIR_RES * DIR_RES
 
 
