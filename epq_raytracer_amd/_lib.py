@@ -104,7 +104,7 @@ EXPORTED_SYMBOLS = (
     "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory",
     "hrt_stream", "hrt_last_error",
     "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
-    "hrt_debug_bvh_build",
+    "hrt_debug_bvh_build", "hrt_debug_bvh_wq_nodes",
     "hrt_obj_load", "hrt_obj_num_meshes", "hrt_obj_mesh", "hrt_obj_free",
 )
 
@@ -155,6 +155,7 @@ def load() -> ctypes.CDLL:
         "hrt_debug_unmap_memory": (c_int32, [P, c_uint64]),
         "hrt_debug_bvh_build": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, P, c_uint64, P, c_uint64, P,
                                           c_uint64, P, c_uint64, P, c_uint64]),
+        "hrt_debug_bvh_wq_nodes": (c_int64, [P, c_uint32, P, c_uint32, c_uint32, P, c_uint64]),
         "hrt_host_ray_grid": (c_uint32, [c_uint32, c_uint32, c_float, c_float, POINTER(c_float), POINTER(c_float),
                                          POINTER(c_float), POINTER(c_float), POINTER(c_float)]),
         "hrt_set_option": (c_int32, [P, c_uint32, c_int64]),

@@ -74,6 +74,7 @@ struct hrt_context {
   float4* cam_tris = nullptr;     // compacted camera-facing records (64 B each)
   float4* cam_cull = nullptr;     // bundle-cull records (80 B each)
   float4* bvh_nodes = nullptr;    // BUNDLE_BVH hierarchy (hrt_bvh.h), built by hrt_set_scene
+  float4* bvh_wq_nodes = nullptr; // its 48 B node image for BUNDLE_WQ (nullptr above 65535 nodes)
   float4* bvh_prims = nullptr;
   float4* bvh_irregular = nullptr;
   uint32_t* bvh_band_off = nullptr;
@@ -263,6 +264,7 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
   free_dev(ctx->cam_tris);
   free_dev(ctx->cam_cull);
   free_dev(ctx->bvh_nodes);
+  free_dev(ctx->bvh_wq_nodes);
   free_dev(ctx->bvh_prims);
   free_dev(ctx->bvh_irregular);
   free_dev(ctx->bvh_band_off);
@@ -338,6 +340,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   hrt::BvhHost bvh;
   const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, ctx->bvh_leaf, bvh);
   free_dev(ctx->bvh_nodes);
+  free_dev(ctx->bvh_wq_nodes);
   free_dev(ctx->bvh_prims);
   free_dev(ctx->bvh_irregular);
   free_dev(ctx->bvh_band_off);
@@ -352,6 +355,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
       return HRT_OK;
     };
     if ((st = up(ctx->bvh_nodes, bvh.nodes)) != HRT_OK) return st;
+    if (bvh.wq_ok && (st = up(ctx->bvh_wq_nodes, bvh.wq_nodes)) != HRT_OK) return st;
     if ((st = up(ctx->bvh_prims, bvh.prims)) != HRT_OK) return st;
     if ((st = up(ctx->bvh_irregular, bvh.irregular)) != HRT_OK) return st;
     if ((st = up(ctx->bvh_band_off, bvh.band_off)) != HRT_OK) return st;
@@ -430,6 +434,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.plan_valid = ctx->plan_valid ? 1u : 0u;
   p.num_cus = ctx->grid_cus ? std::min(ctx->grid_cus, ctx->num_cus) : ctx->num_cus;
   p.bvh_nodes = ctx->bvh_info[4] ? ctx->bvh_nodes : nullptr;
+  p.bvh_wq_nodes = ctx->bvh_info[4] ? ctx->bvh_wq_nodes : nullptr;
   p.bvh_prims = ctx->bvh_prims;
   p.bvh_irregular = ctx->bvh_irregular;
   p.bvh_band_off = ctx->bvh_band_off;

@@ -309,7 +309,52 @@ void build_band_lists(BvhHost& out) {
   }
 }
 
+// Every finite binary16 value (ascending, +0 once) with its bits: directed conversions by search.
+struct Half {
+  std::vector<std::pair<double, uint16_t>> v;
+  Half() {
+    for (uint32_t b = 0; b < 0x10000u; ++b) {
+      const uint32_t e = (b >> 10) & 31u, m = b & 1023u;
+      if (e == 31u || b == 0x8000u) continue;  // inf / NaN, -0
+      const double mag = e ? std::ldexp(1024.0 + m, (int)e - 25) : std::ldexp((double)m, -24);
+      v.emplace_back((b >> 15) ? -mag : mag, (uint16_t)b);
+    }
+    std::sort(v.begin(), v.end());
+  }
+  // dir < 0: largest value <= x; dir > 0: smallest >= x; 0: nearest (ties to the lower)
+  uint16_t conv(double x, int dir) const {
+    x = std::max(v.front().first, std::min(v.back().first, x));
+    size_t i = (size_t)(std::lower_bound(v.begin(), v.end(), std::make_pair(x, (uint16_t)0)) - v.begin());
+    if (i == v.size()) i = v.size() - 1;
+    if (dir > 0) return v[i].second;                      // v[i] >= x
+    if (v[i].first == x || i == 0) return v[i].second;
+    if (dir < 0) return v[i - 1].second;                  // v[i - 1] < x
+    return (x - v[i - 1].first <= v[i].first - x) ? v[i - 1].second : v[i].second;
+  }
+};
+
 }  // namespace
+
+bool make_wq_nodes(const BvhHost& b, std::vector<float>& out) {
+  out.clear();
+  if (b.n_nodes >= 0x10000u) return false;
+  static const Half h;
+  out.resize((size_t)b.n_nodes * 12);
+  for (uint32_t k = 0; k < b.n_nodes; ++k) {
+    const float* r = &b.nodes[(size_t)k * 16];
+    float* w = &out[(size_t)k * 12];
+    for (int j = 0; j < 8; ++j) w[j] = r[j];
+    uint32_t u[4];
+    std::memcpy(&u[3], &r[14], 4);  // leaf info / right child
+    uint32_t esc;
+    std::memcpy(&esc, &r[15], 4);
+    u[0] = h.conv(r[8], 0) | (uint32_t)h.conv(r[9], 0) << 16;
+    u[1] = h.conv(r[10], 0) | (uint32_t)h.conv(r[11], -1) << 16;
+    u[2] = h.conv(r[12], +1) | esc << 16;
+    std::memcpy(&w[8], u, 16);
+  }
+  return true;
+}
 
 bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
                uint32_t leaf_size, BvhHost& out) {
@@ -378,6 +423,7 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
   const double e = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)kBandTau - out.rho_max - 4e-7);
   out.abs_coef = round_up(2.1 * (4.2 * e + out.rho_max) * inv_tp * (1.0 + 1e-6));
   out.rel_t = round_up((2.1 * (3.2 * e + out.rho_max) * inv_tp + 4 * e) * (1.0 + 1e-6));
+  out.wq_ok = make_wq_nodes(out, out.wq_nodes);
   return true;
 }
 
@@ -406,4 +452,13 @@ extern "C" int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, co
                   copy(irregular, irregular_cap, b.irregular) && copy(band_off, band_off_cap, b.band_off) &&
                   copy(band_list, band_list_cap, b.band_list);
   return ok ? 1 : -1;
+}
+
+extern "C" int64_t hrt_debug_bvh_wq_nodes(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes,
+                                          uint32_t n_meshes, uint32_t leaf_size, float* out, uint64_t cap) {
+  hrt::BvhHost b;
+  if (!hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf_size, b) || !b.wq_ok || b.wq_nodes.empty()) return 0;
+  if (!out || cap < b.wq_nodes.size()) return -1;
+  std::memcpy(out, b.wq_nodes.data(), b.wq_nodes.size() * sizeof(float));
+  return (int64_t)(b.wq_nodes.size() / 12);
 }

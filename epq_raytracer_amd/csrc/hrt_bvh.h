@@ -40,6 +40,8 @@ struct BvhHost {
   std::vector<uint32_t> key_base;   // per mesh: scan key of (m, i) = key_base[m] + i (mod 2^32)
   std::vector<uint32_t> band_off;   // 6 kDirRes^2 + 1 offsets into band_list
   std::vector<uint32_t> band_list;  // 4 words per entry: n^ (3 floats, rounded), prim index
+  std::vector<float> wq_nodes;      // BUNDLE_WQ's 48 B node image (make_wq_nodes)
+  bool wq_ok = false;               // the image exists (at most 65535 nodes)
   uint32_t n_nodes = 0, n_prims = 0, n_irregular = 0, n_never = 0;  // never = zero normal (dn == 0)
   double rho_max = 0.0;
   float abs_coef = 0.0f, rel_t = 0.0f;  // box-test t-slack: [-abs_coef R, best (1 + rel_t) + abs_coef R]
@@ -54,6 +56,17 @@ constexpr uint32_t kBvhMaxLeafCount = 16;  // leaf count lives in bits 27..31 of
 // The grazing-band lists hold ~450 entries (16 B) per triangle on the reference's meshes, so the
 // hierarchy is not built above this many (mesh, triangle) entries (~1.9 GB of band lists).
 constexpr uint64_t kBvhMaxEntries = 1u << 18;
+
+// BUNDLE_WQ node image, 12 floats per node (48 B instead of 64, so cave-sized hierarchies leave
+// room for the pair stacks in LDS):
+//   [0..2] box lo, [3] margin a, [4..6] box hi, [7] margin b   (as in the full node)
+//   [8]  bits: cone axis x | axis y << 16   (binary16, nearest: |error| <= 2^-12 per component)
+//   [9]  bits: cone axis z | cos(phi) << 16 (cos rounded down)
+//   [10] bits: sin(phi) (rounded up) | escape node << 16
+//   [11] bits: leaf ? first_prim | count << 27 : right child
+// The kernel widens its back-face cone test by the axis error, so the image only ever keeps more.
+constexpr float kWqAxisErr = 5e-4f;  // >= sqrt(3) 2^-12: bound on |d.axis_16 - d.axis| for |d| = 1
+bool make_wq_nodes(const BvhHost& b, std::vector<float>& out);
 
 // Builds the hierarchy over every (mesh, triangle) entry of the scene.  Returns false (and leaves
 // `out` empty) when the scene has more than kBvhMaxMeshes meshes, kBvhMaxEntries entries or 2^26

@@ -1140,15 +1140,29 @@ __device__ __forceinline__ f3 shfl3(f3 v, uint32_t r) {
   return mk(__shfl(v.x, (int)r, 64), __shfl(v.y, (int)r, 64), __shfl(v.z, (int)r, 64));
 }
 
-// bvh_node_visit with the hardware square root (1 ulp; the extra 2e-7 keeps the cone's sine an upper
-// bound, so a node is only ever kept more often) and the box entry distance for ordering.
+// BUNDLE_WQ node image (hrt_bvh.h make_wq_nodes): 3 float4 per node, cone in binary16.
+__device__ __forceinline__ float half_lo(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xFFFFu)); }
+__device__ __forceinline__ float half_hi(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); }
+__device__ __forceinline__ uint32_t wq_info(const float4* nodes, uint32_t k) {  // leaf info / right child
+  return __builtin_bit_cast(uint32_t, nodes[3 * k + 2].w);
+}
+__device__ __forceinline__ uint32_t wq_escape(const float4* nodes, uint32_t k) {
+  return __builtin_bit_cast(uint32_t, nodes[3 * k + 2].z) >> 16;
+}
+
+// bvh_node_visit on the 48 B image: the cone axis carries up to kWqAxisErr of binary16 error in d.axis
+// (allowed for in both the back-face bound and the sine bound; cos is rounded down and sin up), and
+// the hardware square root (1 ulp; +2e-7 keeps the sine an upper bound) -- a node is only ever kept
+// more often than by bvh_node_visit.  t_near: the box entry distance (ordering only).
 __device__ __forceinline__ bool wq_node_visit(const float4* nd, f3 o, f3 d, f3 inv, float R, float abs_t, float t_hi,
                                               float& t_near) {
-  const float4 N0 = nd[0], N1 = nd[1], N2 = nd[2], N3 = nd[3];
-  const float x = N2.x * d.x + N2.y * d.y + N2.z * d.z;
-  const float xa = fmaxf(fabsf(x) - 2e-6f, 0.0f);
+  const float4 N0 = nd[0], N1 = nd[1], N2 = nd[2];
+  const uint32_t w8 = __builtin_bit_cast(uint32_t, N2.x), w9 = __builtin_bit_cast(uint32_t, N2.y),
+                 w10 = __builtin_bit_cast(uint32_t, N2.z);
+  const float x = half_lo(w8) * d.x + half_hi(w8) * d.y + half_lo(w9) * d.z;
+  const float xa = fmaxf(fabsf(x) - (2e-6f + kWqAxisErr), 0.0f);
   const float s_up = __builtin_amdgcn_sqrtf(fmaxf(1.0f - xa * xa, 0.0f)) + 1.2e-6f;
-  if (x * N2.w - s_up * N3.x - 1e-6f > 1e-5f) return false;  // back: every dn > 0
+  if ((x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back: every dn > 0
   const float mg = N0.w + N1.w * R;
   const float tx0 = ((N0.x - mg) - o.x) * inv.x, tx1 = ((N1.x + mg) - o.x) * inv.x;
   const float ty0 = ((N0.y - mg) - o.y) * inv.y, ty1 = ((N1.y + mg) - o.y) * inv.y;
@@ -1274,7 +1288,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   bool rvis = false;
   if (sec && mask) {
     float tn;
-    rinfo = __builtin_bit_cast(uint32_t, wq.nodes[3].z);
+    rinfo = wq_info(wq.nodes, 0);
     rvis = wq_node_visit(wq.nodes, o, d, inv, R, abs_t, c.t * (1.0f + P.bvh_rel_t) + abs_t, tn);
   }
   const uint32_t rcnt = rvis ? rinfo >> 27 : 0u;
@@ -1326,15 +1340,13 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (is_node) {
       const uint32_t p = e >> 6;
-      const float4 P3 = wq.nodes[4 * p + 3];
-      const uint32_t cr = __builtin_bit_cast(uint32_t, P3.z);  // right child; the left one is p + 1
+      const uint32_t cr = wq_info(wq.nodes, p);  // right child; the left one is p + 1
       if (!overflow) {
         bool sv[4] = {true, true, false, false};
         sn[0] = p + 1u;
         sn[1] = cr;
         if (deep) {
-          const uint32_t il = __builtin_bit_cast(uint32_t, wq.nodes[4 * (p + 1) + 3].z);
-          const uint32_t ir = __builtin_bit_cast(uint32_t, wq.nodes[4 * cr + 3].z);
+          const uint32_t il = wq_info(wq.nodes, p + 1), ir = wq_info(wq.nodes, cr);
           sn[2] = cr;
           sv[2] = true;
           sv[1] = false;
@@ -1353,8 +1365,8 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (sv[k]) {
-            si[k] = __builtin_bit_cast(uint32_t, wq.nodes[4 * sn[k] + 3].z);
-            sk[k] = wq_node_visit(wq.nodes + 4 * sn[k], ro, rd, rinv, rR, rabs, t_hi, st[k]);
+            si[k] = wq_info(wq.nodes, sn[k]);
+            sk[k] = wq_node_visit(wq.nodes + 3 * sn[k], ro, rd, rinv, rR, rabs, t_hi, st[k]);
           }
         }
         // two children: the nearer one in slot 1, pushed above every lane's slot-0 entries (popped first)
@@ -1366,18 +1378,18 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
           sn[1] = tnode; si[1] = tinfo; sk[1] = tk; st[1] = tt;
         }
       } else {  // finish p's subtree below p with a stackless walk (escape links)
-        const uint32_t end = __builtin_bit_cast(uint32_t, P3.w);
+        const uint32_t end = wq_escape(wq.nodes, p);
         uint32_t cur = p + 1;
         while (cur < end) {
-          const uint32_t inf = __builtin_bit_cast(uint32_t, wq.nodes[4 * cur + 3].z), cnt = inf >> 27;
+          const uint32_t inf = wq_info(wq.nodes, cur), cnt = inf >> 27;
           float tnear;
           const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
-          const bool v = wq_node_visit(wq.nodes + 4 * cur, ro, rd, rinv, rR, rabs, t_hi, tnear);
+          const bool v = wq_node_visit(wq.nodes + 3 * cur, ro, rd, rinv, rR, rabs, t_hi, tnear);
           if (v && cnt) {
             const uint32_t first = inf & 0x07FFFFFFu;
             for (uint32_t k = first; k < first + cnt; ++k) wq_leaf_prim(P, wq, k, r, rm, ro, rd);
           }
-          cur = (v && !cnt) ? cur + 1 : __builtin_bit_cast(uint32_t, wq.nodes[4 * cur + 3].w);
+          cur = (v && !cnt) ? cur + 1 : wq_escape(wq.nodes, cur);
         }
       }
     }
@@ -1809,13 +1821,13 @@ __global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
 }
 
 // BUNDLE_WQ: the hierarchy's nodes in LDS, one pair-stack region per wave after them (persistent
-// 1024-thread workgroups).  Dynamic LDS: [nodes x 64 B][16 x (64 slots x 8 B, wq_ncap + wq_tcap words)].
+// 1024-thread workgroups).  Dynamic LDS: [nodes x 48 B][16 x (64 slots x 8 B, wq_ncap + wq_tcap words)].
 template <bool D>
 __global__ __launch_bounds__(1024) void trace_bundle_wq(TraceParams P) {
   const uint32_t nn = P.bvh_n_nodes;
   float4* nodes = lds_tris;
-  for (uint32_t k = threadIdx.x; k < 4 * nn; k += 1024) nodes[k] = P.bvh_nodes[k];
-  char* base = reinterpret_cast<char*>(nodes + 4 * nn) + (size_t)(threadIdx.x >> 6) * (512 + 4 * (P.wq_ncap + P.wq_tcap));
+  for (uint32_t k = threadIdx.x; k < 3 * nn; k += 1024) nodes[k] = P.bvh_wq_nodes[k];
+  char* base = reinterpret_cast<char*>(nodes + 3 * nn) + (size_t)(threadIdx.x >> 6) * (512 + 4 * (P.wq_ncap + P.wq_tcap));
   const WqLds wq{nodes, reinterpret_cast<unsigned long long*>(base), reinterpret_cast<uint32_t*>(base + 512),
                  reinterpret_cast<uint32_t*>(base + 512) + P.wq_ncap, P.wq_ncap};
   __syncthreads();
@@ -2001,8 +2013,8 @@ uint32_t lds_block(uint32_t n) {
 // BUNDLE_WQ per-wave pair stacks: triangle stack 64 x (1 + 2 x largest leaf), node stack what is left of
 // the 160 KiB after the nodes (at most 1024 pairs, at least 128).  Returns the LDS bytes, 0 = no fit.
 size_t wq_lds_bytes(const TraceParams& p, uint32_t* ncap, uint32_t* tcap) {
-  if (!p.bvh_nodes || p.bvh_max_leaf > 4) return 0;
-  const size_t nodes = (size_t)p.bvh_n_nodes * 64, t = 64u * (1u + 2u * p.bvh_max_leaf);
+  if (!p.bvh_nodes || !p.bvh_wq_nodes || p.bvh_max_leaf > 4) return 0;
+  const size_t nodes = (size_t)p.bvh_n_nodes * 48, t = 64u * (1u + 2u * p.bvh_max_leaf);
   if (nodes + 16 * (512 + 4 * (t + 128)) > kMaxLdsScene) return 0;
   const size_t per_wave = (kMaxLdsScene - nodes) / 16;
   const uint32_t n = (uint32_t)std::min<size_t>(1024, ((per_wave - 512 - 4 * t) / 4) & ~(size_t)63);
@@ -2014,10 +2026,10 @@ size_t wq_lds_bytes(const TraceParams& p, uint32_t* ncap, uint32_t* tcap) {
 int resolve_variant(const TraceParams& p, int variant) {
   if (variant == HRT_KERNEL_AUTO) {
     // profiles/r01g_*: island 21.4 (LDS) vs 23.7 ms, cave 112 vs 120 ms; BVH from ~4K triangles.
-    // BUNDLE_WQ when its node stacks get >= 512 pairs (profiles/r01m_*: island 8.1 vs 15.6 ms; with
-    // 192 (cave) the stackless fallback runs too often: 60-78 vs 31 ms)
+    // BUNDLE_WQ when its node stacks get >= 768 pairs (profiles/r01m_*: island, 1,024 pairs, 8.1 vs
+    // 15.6 ms; cave, 576 pairs with the 48 B node image: 36-39 vs 31-34 ms, r01o)
     uint32_t ncap = 0;
-    const bool wq = wq_lds_bytes(p, &ncap, nullptr) && ncap >= 512 && p.pc.num_meshes <= 64;
+    const bool wq = wq_lds_bytes(p, &ncap, nullptr) && ncap >= 768 && p.pc.num_meshes <= 64;
     variant = p.cam_list_capacity < kAutoCullTris                   ? HRT_KERNEL_BUNDLE
               : wq                                                 ? HRT_KERNEL_BUNDLE_WQ
               : p.cam_list_capacity >= kAutoBvhTris && p.bvh_nodes ? HRT_KERNEL_BUNDLE_BVH

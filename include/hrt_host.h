@@ -37,13 +37,19 @@ uint32_t hrt_host_ray_grid(uint32_t width, uint32_t height, float camera_focal_l
 
 /* Host-only inspection of the hierarchy hrt_set_scene builds for BUNDLE_BVH (tests; no GPU).
  * counts = {nodes, prims, irregular, never, built, band entries}; each array (capacity in elements:
- * floats for nodes/prims/irregular = 16 per record, u32 for band_off = 6*64*64+1 and band_list =
+ * floats for nodes/prims/irregular = 16 per record, u32 for band_off = 6*128*128+1 and band_list =
  * 4 per entry) is filled when non-NULL and large enough.  Returns 1 (filled), 0 (not built),
  * -1 (a capacity too small). */
 int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
                         uint32_t leaf_size, uint32_t counts[6], float* nodes, uint64_t nodes_cap, float* prims,
                         uint64_t prims_cap, float* irregular, uint64_t irregular_cap, uint32_t* band_off,
                         uint64_t band_off_cap, uint32_t* band_list, uint64_t band_list_cap);
+
+/* Host-only: the 48-byte node image BUNDLE_WQ stages in LDS (12 floats per node, layout in
+ * epq_raytracer_amd/csrc/hrt_bvh.h make_wq_nodes) for the hierarchy hrt_set_scene would build.
+ * Returns the node count (out filled), 0 (not built / above 65535 nodes), -1 (cap too small). */
+int64_t hrt_debug_bvh_wq_nodes(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
+                               uint32_t leaf_size, float* out, uint64_t cap);
 
 /* Column-major mat4 for push_constants.cam_alignment_mat: columns = normalised direction,
  * new_y, new_z (so mat3(M) * (1,0,0) = direction / |direction|), 4th column (0,0,0,1). */

@@ -236,3 +236,34 @@ def test_leaf_sizes(leaf):
     b = build(case.tris, case.meshes, leaf)
     counts = (b["nodes"].view(np.uint32)[:, 14] >> 27)
     assert counts.max() <= leaf and counts.sum() == len(b["prims"])
+
+
+@pytest.mark.parametrize("scene", ["island", "cave", "box"])
+def test_wq_node_image(scene):
+    """BUNDLE_WQ's 48 B node image (hrt_bvh.h make_wq_nodes) against the full nodes: boxes, margins,
+    leaf info / right child and escape copied exactly; the binary16 cone only ever widens (cos
+    rounded down, sin up) and the axis is within 2^-12 per component (kernel allows 5e-4 in d.axis)."""
+    case = SceneCase(scene, (8, 8), 1, 1)
+    b = build(case.tris, case.meshes, 4)
+    if b is None:
+        return
+    lib = _lib.load()
+    nn = len(b["nodes"])
+    img = np.zeros(nn * 12, np.float32)
+    got = lib.hrt_debug_bvh_wq_nodes(case.tris.ctypes.data, len(case.tris), case.meshes.ctypes.data,
+                                     len(case.meshes), 4, img.ctypes.data, img.size)
+    assert got == nn
+    img = img.reshape(nn, 12)
+    N = b["nodes"]
+    np.testing.assert_array_equal(bits(img[:, 0:8]), bits(N[:, 0:8]))
+    w = bits(img[:, 8:12])
+    np.testing.assert_array_equal(w[:, 3], bits(N[:, 14]))                 # leaf info / right child
+    np.testing.assert_array_equal(w[:, 2] >> 16, bits(N[:, 15]))           # escape
+    half = lambda u: (u & 0xFFFF).astype(np.uint16).view(np.float16).astype(np.float64)
+    ax, ay, az = half(w[:, 0]), half(w[:, 0] >> 16), half(w[:, 1])
+    cq, sq = half(w[:, 1] >> 16), half(w[:, 2])
+    axis = N[:, 8:11].astype(np.float64)
+    assert np.abs(np.stack([ax, ay, az], 1) - axis).max() <= 2.0 ** -12
+    assert (cq <= N[:, 11].astype(np.float64)).all() and (cq >= 0).all()
+    assert (sq >= N[:, 12].astype(np.float64)).all()
+    assert np.linalg.norm(np.stack([ax, ay, az], 1) - axis, axis=1).max() <= 5e-4  # |d.(A16 - A)| <= |A16 - A|
