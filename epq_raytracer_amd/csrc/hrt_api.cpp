@@ -61,7 +61,7 @@ struct hrt_context {
   unsigned long long* tile_cycles = nullptr;  // diagnostics: shader clocks per 8x8 tile of the last trace
   uint32_t* sched = nullptr;      // persistent kernels' scheduler words (hrt_kernels.h)
   uint32_t* tile_cost = nullptr;  // per 8x8 tile
-  uint32_t* item_buf = nullptr;   // planned work items (tiles x 8)
+  uint32_t* item_buf = nullptr;   // planned work items (tiles x 64: a heavy tile runs as up to 64 items)
   bool plan_valid = false;        // tile_cost describes the last trace (same size, persistent kernel)
   uint32_t split_k = 0, split_prio = 1;  // split 0: auto (per kernel, launch_trace)
   int32_t split_factor = -1;  // auto
@@ -224,7 +224,7 @@ extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_
     if ((e = hipMalloc((void**)&ctx->sched, 256 * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(sched)"));
     if ((e = hipMalloc((void**)&ctx->tile_cost, (tiles ? tiles : 1) * 4)) != hipSuccess)
       return bail(hip_fail(ctx, e, "hipMalloc(tile costs)"));
-    if ((e = hipMalloc((void**)&ctx->item_buf, (tiles ? tiles : 1) * 8 * 4)) != hipSuccess)
+    if ((e = hipMalloc((void**)&ctx->item_buf, (tiles ? tiles : 1) * 64 * 4)) != hipSuccess)
       return bail(hip_fail(ctx, e, "hipMalloc(items)"));
   }
   {
@@ -721,8 +721,8 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       ctx->sec_batch = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_SPLIT:
-      if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
-        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "split must be 0 (auto), 1, 2, 4 or 8");
+      if (value < 0 || value > 64 || (value & (value - 1)) != 0)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "split must be 0 (auto) or a power of two up to 64");
       ctx->split_k = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_SPLIT_FACTOR:

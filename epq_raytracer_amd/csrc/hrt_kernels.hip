@@ -1125,6 +1125,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // without vs 8.2-8.3 ms with 32 on island, no gain on one rank of 8 (profiles/r01n_wq_ab.txt)
 #define HRT_WQ_DEEP 0u
 #endif
+#ifndef HRT_WQ_CONE
+#define HRT_WQ_CONE 1    // the nodes' back-face (normal cone) test
+#endif
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
 #endif
@@ -1162,7 +1165,7 @@ __device__ __forceinline__ bool wq_node_visit(const float4* nd, f3 o, f3 d, f3 i
   const float x = half_lo(w8) * d.x + half_hi(w8) * d.y + half_lo(w9) * d.z;
   const float xa = fmaxf(fabsf(x) - (2e-6f + kWqAxisErr), 0.0f);
   const float s_up = __builtin_amdgcn_sqrtf(fmaxf(1.0f - xa * xa, 0.0f)) + 1.2e-6f;
-  if ((x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back: every dn > 0
+  if (HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back
   const float mg = N0.w + N1.w * R;
   const float tx0 = ((N0.x - mg) - o.x) * inv.x, tx1 = ((N1.x + mg) - o.x) * inv.x;
   const float ty0 = ((N0.y - mg) - o.y) * inv.y, ty1 = ((N1.y + mg) - o.y) * inv.y;
@@ -1637,14 +1640,16 @@ __device__ __forceinline__ void stage_tris(const TraceParams& P, float4* dst, ui
 // is done, so no wave idles while a slower wave of its workgroup finishes.  Every wave leaves the
 // loop once the counter passes the tile count.
 //
-// Work items (P.items, built by plan_fill from the previous trace's per-tile costs): tile | sub << 25
-// | log2 K << 29 | heavy << 31.  sub == 0 is a whole tile; sub = 1..K covers rows [(sub-1) * 8/K,
-// sub * 8/K) of a heavy tile with 64/K lanes (the rest idle); K grows with the tile's cost.  A heavy tile's pixels run as K shorter sample chains in parallel
+// Work items (P.items, built by plan_fill from the previous trace's per-tile costs): tile | log2 K << 22
+// | s << 25 | heavy << 31.  K == 1 is a whole tile; otherwise item s (0..K-1) covers the tile's pixels
+// [s * 64/K, (s+1) * 64/K) in row-major order with 64/K lanes (the rest idle); K (2..64) grows with
+// the tile's cost.  A heavy tile's pixels run as K shorter sample chains in parallel
 // with lighter batches, and the planner puts them first.  Every pixel is computed exactly once and
 // independently of which wave runs it, so the bytes do not depend on the plan.  Each item's cost goes
 // to P.tile_cost[tile] for the next plan: deterministic work units (Coop::work: survivor tests,
 // culled chunks, primary list entries, iterations; the same with or without cooperation) in
 // BUNDLE_CULL_LDS, shader clocks / 16 in BUNDLE_BVH_LDS.
+constexpr uint32_t kItemTileMask = (1u << 22) - 1u;  // planned traces need fewer than 2^22 tiles
 template <int BLOCK, bool CoopOk, class Body>
 __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long long* ex, uint32_t* s_item, Body&& body) {
   const uint32_t lane = threadIdx.x & 63;
@@ -1671,7 +1676,7 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
       const uint32_t h = __builtin_amdgcn_readfirstlane(*s_item);
       __syncthreads();
       if (h >= H) break;
-      const uint32_t tile = __builtin_amdgcn_readfirstlane(P.items[h]) & 0x01FFFFFFu;
+      const uint32_t tile = __builtin_amdgcn_readfirstlane(P.items[h]) & kItemTileMask;
       const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
       co.work = 0;
       body(tx * 8 + (lane & 7), ty * 8 + (lane >> 3), co);
@@ -1700,18 +1705,13 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     }
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= n) break;
-    const uint32_t item = __builtin_amdgcn_readfirstlane(P.items ? P.items[t] : t);
-    const uint32_t tile = item & 0x01FFFFFFu, sub = (item >> 25) & 15u, lk = (item >> 29) & 3u;
+    const uint32_t item = P.items ? __builtin_amdgcn_readfirstlane(P.items[t]) : 0u;
+    const uint32_t tile = P.items ? item & kItemTileMask : t, lk = (item >> 22) & 7u, sub = (item >> 25) & 63u;
     const bool hot = item >> 31;  // heavy last time: issue priority over the light tiles' waves
     const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
-    uint32_t x = tx * 8 + (lane & 7), lr = ty * 8 + (lane >> 3);
-    if (sub) {
-      const uint32_t rows = 8u >> lk, r = lane >> 3;
-      if (r < rows)
-        lr = ty * 8 + (sub - 1) * rows + r;
-      else
-        x = 0xFFFFFFFFu;  // idle lane
-    }
+    const uint32_t j = (sub << (6u - lk)) + lane;  // the tile pixel (row-major) of this lane
+    uint32_t x = tx * 8 + (j & 7u), lr = ty * 8 + (j >> 3);
+    if (lane >= (64u >> lk)) x = 0xFFFFFFFFu;  // idle lane of a split item
     const uint64_t t0 = __builtin_readcyclecounter();
     if (hot) __builtin_amdgcn_s_setprio(3);
     solo.work = 0;
@@ -1752,10 +1752,10 @@ __global__ __launch_bounds__(256) void plan_hist(uint32_t* sched, const uint32_t
   __syncthreads();
   if (threadIdx.x < kPlanBuckets && h[threadIdx.x]) atomicAdd(&sched[8 + threadIdx.x], h[threadIdx.x]);
 }
-// Items of a heavy tile in bucket b >= hb: 2 per half-octave pair above the threshold, doubling
-// (costs [1, 2) x threshold: 2 items, [2, 4): 4, then 8), at most kmax; kmax = 1: never split.
+// Items of a heavy tile in bucket b >= hb: doubling per octave above the threshold (costs [1, 2) x
+// threshold: 2 items, [2, 4): 4, ... up to 64 single pixels), at most kmax; kmax = 1: never split.
 __device__ __forceinline__ uint32_t bucket_items(uint32_t b, uint32_t hb, uint32_t kmax) {
-  return b < hb ? 1u : min(kmax, 2u << min((b - hb) >> 1, 2u));
+  return b < hb ? 1u : min(kmax, 2u << min((b - hb) >> 1, 5u));
 }
 __global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves, uint32_t factor, uint32_t kmax,
                                                 uint32_t prio) {
@@ -1774,7 +1774,7 @@ __global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves,
   sched[2] = heavy;
   sched[3] = hb;
 }
-// Item word: tile | sub << 25 (1..8, 0 = whole tile) | log2(items of the tile) << 29 | heavy << 31.
+// Item word: tile | log2(items of the tile) << 22 | item index s << 25 | heavy << 31 (tile_loop).
 __global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t* cost, uint32_t tiles, uint32_t kmax,
                                                  uint32_t prio, uint32_t* items) {
   __shared__ uint32_t cnt[kPlanBuckets], base[kPlanBuckets];
@@ -1800,7 +1800,7 @@ __global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t
       items[at] = i | flag;
     } else {
       const uint32_t lk = (uint32_t)__builtin_ctz(k);
-      for (uint32_t s = 0; s < k; ++s) items[at + s] = i | ((s + 1) << 25) | (lk << 29) | flag;
+      for (uint32_t s = 0; s < k; ++s) items[at + s] = i | (lk << 22) | (s << 25) | flag;
     }
   }
 }
@@ -2051,7 +2051,8 @@ int resolve_variant(const TraceParams& p, int variant) {
 // splitting is on), then reset the counters the trace fills.  q.items = nullptr: plain tile order.
 static hipError_t prepare_schedule(TraceParams& q, hipStream_t stream) {
   const uint32_t tiles = ((q.pc.width + 7) / 8) * ((q.local_rows + 7) / 8);
-  const bool plan = q.plan_valid && tiles > 0;  // longest-first order whenever last trace's costs are known
+  // longest-first order whenever last trace's costs are known (and tile indices fit the item word)
+  const bool plan = q.plan_valid && tiles > 0 && tiles <= kItemTileMask;
   q.items = plan ? q.item_buf : nullptr;
   hipError_t e;
   if (plan) {

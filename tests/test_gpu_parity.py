@@ -54,7 +54,7 @@ def test_every_variant_bit_exact(scene, size, spp, bounces, variant):
 
 
 @pytest.mark.parametrize("split,factor,prio", [(1, 4, 0), (1, 4, 1), (1, 0, 1), (2, 0, 0), (4, 0, 1), (8, 0, 0),
-                                               (4, 4, 1), (8, 2, 1)])
+                                               (4, 4, 1), (8, 2, 1), (16, 0, 1), (64, 0, 0), (0, -1, 1)])
 @pytest.mark.parametrize("scene,size,spp,bounces,variant", [("cave", (64, 48), 2, 8, 7), ("island", (75, 41), 3, 8, 7),
                                                             ("island", (75, 41), 3, 8, 8), ("island", (75, 41), 3, 8, 9),
                                                             ("cave", (64, 48), 2, 8, 9)])
@@ -123,7 +123,7 @@ def test_coop_tiles_bit_exact(scene, factor):
 
 
 @pytest.mark.parametrize("cap", [0, 128])
-@pytest.mark.parametrize("split", [0, 1])
+@pytest.mark.parametrize("split", [0, 1, 64])
 @pytest.mark.parametrize("scene", ["island", "cave", "box", "spheres", "ties"])
 def test_wq_pairs_bit_exact(scene, split, cap):
     """BUNDLE_WQ: bounce rays through the hierarchy as (ray, node) / (ray, triangle) pairs on per-wave
@@ -181,7 +181,7 @@ def test_split_schedule_partition_and_scene_change(split, coop, variant):
 def test_split_options_validated():
     case = SceneCase("box", (16, 16), 1, 1)
     ctx = case.context(variant=7)
-    for bad in (-1, 3, 16):
+    for bad in (-1, 3, 128):
         with pytest.raises(Exception):
             ctx.set_option(_lib.OPT_SPLIT, bad)
     ctx.set_option(_lib.OPT_SPLIT, 0)  # auto
