@@ -72,7 +72,7 @@ MODE_RGBA8, MODE_RGBA32F = 0, 1
 IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
-OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP, OPT_WQ_NODE_CAP = 5, 6, 7, 8, 9, 10
+OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP, OPT_WQ_NODE_CAP, OPT_PROBE = 5, 6, 7, 8, 9, 10, 11
 # hrt_kernel (include/hip_raytrace.h)
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
 KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS, KERNEL_BUNDLE_BVH_LDS, KERNEL_BUNDLE_WQ = 6, 7, 8, 9

@@ -68,6 +68,7 @@ struct hrt_context {
   uint32_t grid_cus = 0;  // HRT_OPT_GRID_CUS (0: every CU)
   uint32_t coop = 1;      // HRT_OPT_COOP
   uint32_t wq_node_cap = 0;  // HRT_OPT_WQ_NODE_CAP (0 = auto)
+  uint32_t probe = 1;        // HRT_OPT_PROBE
   uint32_t num_cus = 0;
   uint32_t* cam_meta = nullptr;   // bundle variants: cam_start[n_meshes], cam_count[n_meshes]
   uint32_t cam_capacity = 0;      // sum of mesh lengths
@@ -458,6 +459,24 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
     HRT_HIP(ctx, hipEventCreate(&ev.start));
     HRT_HIP(ctx, hipEventCreate(&ev.stop));
   }
+  // First trace of a persistent kernel (no tile costs yet): a 1-sample probe trace into the scratch
+  // image measures the tiles' relative costs so that this trace already follows a plan (HRT_OPT_PROBE).
+  const int resolved = hrt::resolve_variant(p, variant);
+  if (ctx->probe && !ctx->plan_valid && ctx->num_tiles() >= 1024 &&
+      (resolved == HRT_KERNEL_BUNDLE_WQ || resolved == HRT_KERNEL_BUNDLE_CULL_LDS ||
+       resolved == HRT_KERNEL_BUNDLE_BVH_LDS)) {
+    hrt::TraceParams q = p;
+    q.pc.num_samples = 1;
+    q.img8 = ctx->trace8 ? reinterpret_cast<uint32_t*>(ctx->scratch) : nullptr;
+    q.img32 = ctx->trace32 ? reinterpret_cast<float4*>(ctx->scratch) : nullptr;
+    q.counters = nullptr;
+    q.diag = nullptr;
+    q.tile_cycles = nullptr;
+    int ran = 0, blk = 0;
+    if (hipError_t pe = hrt::launch_trace(q, variant, ctx->stream, &ran, &blk); pe != hipSuccess)
+      return hip_fail(ctx, pe, "probe trace launch");
+    p.plan_valid = 1u;
+  }
   HRT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
   hipError_t e = hrt::launch_trace(p, variant, ctx->stream, &ctx->last_kernel, &ctx->last_block);
   // the persistent kernels recorded this trace's tile costs: the next one can follow a plan
@@ -733,6 +752,10 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
     case HRT_OPT_PRIORITY:
       if (value < 0 || value > 2) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "priority must be 0, 1 or 2");
       ctx->split_prio = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_PROBE:
+      if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "probe must be 0 or 1");
+      ctx->probe = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_WQ_NODE_CAP:
       if (value != 0 && (value < 128 || value > (1 << 20)))

@@ -205,7 +205,11 @@ typedef enum hrt_option {
   /* BUNDLE_WQ: per-wave node-pair stack capacity (0 = what fits the LDS, default; else at most that,
    * rounded down to a multiple of 64, >= 128).  A step that could overflow it walks its pairs'
    * subtrees stacklessly instead; results do not depend on it (tests force the fallback with 128). */
-  HRT_OPT_WQ_NODE_CAP = 10
+  HRT_OPT_WQ_NODE_CAP = 10,
+  /* persistent kernels: the first trace of a context (no previous tile costs) is preceded by a
+   * 1-sample probe trace into a scratch image whose per-tile costs plan it (1 default, 0 off).
+   * Frames, counters and the trace timing are unaffected. */
+  HRT_OPT_PROBE = 11
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */

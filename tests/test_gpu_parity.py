@@ -178,6 +178,24 @@ def test_split_schedule_partition_and_scene_change(split, coop, variant):
     assert np.array_equal(first[valid], ref[rows[valid]])
 
 
+@pytest.mark.parametrize("variant", [0, 7, 9])
+def test_probe_plan_first_trace(variant):
+    """HRT_OPT_PROBE: the first trace of a persistent kernel (>= 1024 tiles) is planned from a 1-sample
+    probe trace into a scratch image; frames and counters equal the unprobed trace and the oracle."""
+    case = SceneCase("island", (320, 240), 2, 8)
+    ref, _, seg, tt = case.oracle()
+    for probe in (1, 0):
+        ctx = case.context(variant=variant, options={_lib.OPT_PROBE: probe})
+        for _ in range(2):
+            ctx.reset_stats()
+            ctx.trace(case.push())
+            st = ctx.stats()
+            img = ctx.read(_lib.IMG_TRACE)
+            assert np.array_equal(img, ref), f"probe {probe}: " + mismatch_report(img, ref)
+            assert (st.segments, st.tri_tests, st.traces) == (seg, tt, 1)
+        ctx.close()
+
+
 def test_split_options_validated():
     case = SceneCase("box", (16, 16), 1, 1)
     ctx = case.context(variant=7)
@@ -192,6 +210,8 @@ def test_split_options_validated():
         ctx.set_option(_lib.OPT_PRIORITY, 3)
     with pytest.raises(Exception):
         ctx.set_option(_lib.OPT_COOP, 2)
+    with pytest.raises(Exception):
+        ctx.set_option(_lib.OPT_PROBE, 2)
     with pytest.raises(Exception):
         ctx.set_option(_lib.OPT_SPLIT_FACTOR, -2)
     ctx.set_option(_lib.OPT_SPLIT_FACTOR, -1)

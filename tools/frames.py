@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--prio", type=int, default=1)
     ap.add_argument("--split", type=int, default=0)
     ap.add_argument("--ncap", type=int, default=0)
+    ap.add_argument("--probe", type=int, default=1)
     ap.add_argument("--sec-batch", type=int, default=48)
     a = ap.parse_args()
     W, H = (int(v) for v in a.size.split("x"))
@@ -35,7 +36,7 @@ def main():
     ctx = case.context(variant=a.variant, partition=part,
                        options={_lib.OPT_COOP: a.coop, _lib.OPT_SPLIT_FACTOR: a.factor, _lib.OPT_PRIORITY: a.prio,
                                 _lib.OPT_SPLIT: a.split, _lib.OPT_SECONDARY_BATCH: a.sec_batch,
-                                _lib.OPT_WQ_NODE_CAP: a.ncap})
+                                _lib.OPT_WQ_NODE_CAP: a.ncap, _lib.OPT_PROBE: a.probe})
     pc = case.push(1)
     ms = []
     for _ in range(a.frames):
@@ -44,7 +45,7 @@ def main():
         ms.append(round(ctx.stats().total_trace_ms, 3))
     ctx.close()
     print(json.dumps({"scene": a.scene, "variant": a.variant, "partition": a.partition, "coop": a.coop, "factor": a.factor,
-                      "split": a.split, "sec_batch": a.sec_batch, "ncap": a.ncap, "ms": ms}))
+                      "split": a.split, "sec_batch": a.sec_batch, "ncap": a.ncap, "probe": a.probe, "ms": ms}))
 
 
 if __name__ == "__main__":
