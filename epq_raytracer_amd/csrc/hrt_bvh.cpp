@@ -340,17 +340,38 @@ bool make_wq_nodes(const BvhHost& b, std::vector<float>& out) {
   if (b.n_nodes >= 0x10000u) return false;
   static const Half h;
   out.resize((size_t)b.n_nodes * 12);
+  if (b.n_nodes == 0) return true;
+  auto word = [&](uint32_t k, int j) {
+    uint32_t u;
+    std::memcpy(&u, &b.nodes[(size_t)k * 16 + j], 4);
+    return u;
+  };
+  // sibling-adjacent order: root 0, then every inner node's two children at fc, fc + 1
+  std::vector<uint32_t> new_of(b.n_nodes), esc_of(b.n_nodes), first_child(b.n_nodes, 0);
+  new_of[0] = 0;
+  esc_of[0] = b.n_nodes;  // end of the walk
+  uint32_t next = 1;
+  for (uint32_t k = 0; k < b.n_nodes; ++k) {  // preorder: a parent precedes its children
+    if (word(k, 14) >> 27) continue;           // leaf
+    const uint32_t l = k + 1, r = word(k, 14);
+    first_child[k] = next;
+    new_of[l] = next;
+    new_of[r] = next + 1;
+    esc_of[l] = next + 1;       // the left child's escape is its sibling
+    esc_of[r] = esc_of[k];      // the right child's is its parent's
+    next += 2;
+  }
+  if (next != b.n_nodes) return false;  // not a full binary tree (cannot happen: every inner node has 2 children)
   for (uint32_t k = 0; k < b.n_nodes; ++k) {
     const float* r = &b.nodes[(size_t)k * 16];
-    float* w = &out[(size_t)k * 12];
+    float* w = &out[(size_t)new_of[k] * 12];
     for (int j = 0; j < 8; ++j) w[j] = r[j];
+    const uint32_t info = word(k, 14);
     uint32_t u[4];
-    std::memcpy(&u[3], &r[14], 4);  // leaf info / right child
-    uint32_t esc;
-    std::memcpy(&esc, &r[15], 4);
     u[0] = h.conv(r[8], 0) | (uint32_t)h.conv(r[9], 0) << 16;
     u[1] = h.conv(r[10], 0) | (uint32_t)h.conv(r[11], -1) << 16;
-    u[2] = h.conv(r[12], +1) | esc << 16;
+    u[2] = h.conv(r[12], +1) | esc_of[k] << 16;
+    u[3] = (info >> 27) ? info : first_child[k];
     std::memcpy(&w[8], u, 16);
   }
   return true;

@@ -58,12 +58,14 @@ constexpr uint32_t kBvhMaxLeafCount = 16;  // leaf count lives in bits 27..31 of
 constexpr uint64_t kBvhMaxEntries = 1u << 18;
 
 // BUNDLE_WQ node image, 12 floats per node (48 B instead of 64, so cave-sized hierarchies leave
-// room for the pair stacks in LDS):
+// room for the pair stacks in LDS), in sibling-adjacent order: root 0, the two children of an inner
+// node at fc and fc + 1 (a (ray, node pair) needs no parent record):
 //   [0..2] box lo, [3] margin a, [4..6] box hi, [7] margin b   (as in the full node)
 //   [8]  bits: cone axis x | axis y << 16   (binary16, nearest: |error| <= 2^-12 per component)
 //   [9]  bits: cone axis z | cos(phi) << 16 (cos rounded down)
-//   [10] bits: sin(phi) (rounded up) | escape node << 16
-//   [11] bits: leaf ? first_prim | count << 27 : right child
+//   [10] bits: sin(phi) (rounded up) | escape << 16 (left child: its sibling; right child: the
+//        parent's escape; root: n_nodes -- a stackless walk continues there after the subtree)
+//   [11] bits: leaf ? first_prim | count << 27 : first child fc
 // The kernel widens its back-face cone test by the axis error, so the image only ever keeps more.
 constexpr float kWqAxisErr = 5e-4f;  // >= sqrt(3) 2^-12: bound on |d.axis_16 - d.axis| for |d| = 1
 bool make_wq_nodes(const BvhHost& b, std::vector<float>& out);

@@ -1134,7 +1134,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 struct WqLds {
   const float4* nodes;        // BVH nodes (LDS copy)
   unsigned long long* slot;   // 64 per wave: closest hit so far per ray (owner lane)
-  uint32_t* ns;               // node-pair stack: inner node << 6 | ray
+  uint32_t* ns;               // node-pair stack: first node of a sibling pair << 6 | ray
   uint32_t* ts;               // triangle-pair stack: leaf prim << 6 | ray
   uint32_t ncap;              // node stack capacity (>= 256)
 };
@@ -1296,7 +1296,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   }
   const uint32_t rcnt = rvis ? rinfo >> 27 : 0u;
   const unsigned long long rb = __ballot(rvis && rcnt == 0u);
-  if (rvis && rcnt == 0u) wq.ns[lanes_below(rb)] = lane;  // inner root: pair (ray, node 0)
+  if (rvis && rcnt == 0u) wq.ns[lanes_below(rb)] = (rinfo << 6) | lane;  // inner root: its children's pair
   uint32_t nc = (uint32_t)__popcll(rb), tc = 0;
   {  // leaf root (a scene of at most leaf-size triangles): its triangles
     uint32_t pre = 0, tot = 0;
@@ -1331,8 +1331,8 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
     if (is_tri) wq_leaf_prim(P, wq, e >> 6, r, rm, ro, rd);
     if (nn == 0u) continue;
-    // node pairs (ray r, inner node p): test p's children -- or, when few pairs are left (deep, lanes
-    // idle), skip an inner child's own box and test its two children, two levels per step.  Leaving
+    // node pairs (ray r, sibling pair c, c + 1): test both -- or, when few pairs are left (deep, lanes
+    // idle), skip an inner node's own box and test its two children, two levels per step.  Leaving
     // a box untested only ever keeps more.  Slots 0..3 hold the nodes tested by this lane.
     const f3 rinv = shfl3(inv, r);
     const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
@@ -1342,25 +1342,24 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     bool sk[4] = {false, false, false, false};
     float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     if (is_node) {
-      const uint32_t p = e >> 6;
-      const uint32_t cr = wq_info(wq.nodes, p);  // right child; the left one is p + 1
+      const uint32_t c = e >> 6;
       if (!overflow) {
         bool sv[4] = {true, true, false, false};
-        sn[0] = p + 1u;
-        sn[1] = cr;
+        sn[0] = c;
+        sn[1] = c + 1u;
         if (deep) {
-          const uint32_t il = wq_info(wq.nodes, p + 1), ir = wq_info(wq.nodes, cr);
-          sn[2] = cr;
+          const uint32_t il = wq_info(wq.nodes, c), ir = wq_info(wq.nodes, c + 1u);
+          sn[2] = c + 1u;
           sv[2] = true;
           sv[1] = false;
-          if ((il >> 27) == 0u) {  // inner left child: its children instead
-            sn[0] = p + 2u;
-            sn[1] = il;
+          if ((il >> 27) == 0u) {  // inner left node: its children instead
+            sn[0] = il;
+            sn[1] = il + 1u;
             sv[1] = true;
           }
           if ((ir >> 27) == 0u) {
-            sn[2] = cr + 1u;
-            sn[3] = ir;
+            sn[2] = ir;
+            sn[3] = ir + 1u;
             sv[3] = true;
           }
         }
@@ -1380,10 +1379,10 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
           sn[0] = sn[1]; si[0] = si[1]; sk[0] = sk[1]; st[0] = st[1];
           sn[1] = tnode; si[1] = tinfo; sk[1] = tk; st[1] = tt;
         }
-      } else {  // finish p's subtree below p with a stackless walk (escape links)
-        const uint32_t end = wq_escape(wq.nodes, p);
-        uint32_t cur = p + 1;
-        while (cur < end) {
+      } else {  // finish the pair's two subtrees with a stackless walk (escape links)
+        const uint32_t end = wq_escape(wq.nodes, c + 1u);
+        uint32_t cur = c;
+        while (cur != end) {
           const uint32_t inf = wq_info(wq.nodes, cur), cnt = inf >> 27;
           float tnear;
           const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
@@ -1392,7 +1391,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
             const uint32_t first = inf & 0x07FFFFFFu;
             for (uint32_t k = first; k < first + cnt; ++k) wq_leaf_prim(P, wq, k, r, rm, ro, rd);
           }
-          cur = (v && !cnt) ? cur + 1 : wq_escape(wq.nodes, cur);
+          cur = (v && !cnt) ? inf : wq_escape(wq.nodes, cur);  // inner: its first child
         }
       }
     }
@@ -1402,7 +1401,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     for (int k = 0; k < 4; ++k) {
       const bool inner = sk[k] && (si[k] >> 27) == 0u;
       const unsigned long long bk = __ballot(inner);
-      if (inner) wq.ns[nc + lanes_below(bk)] = (sn[k] << 6) | r;
+      if (inner) wq.ns[nc + lanes_below(bk)] = (si[k] << 6) | r;  // the kept node's children pair
       nc += (uint32_t)__popcll(bk);
       cnt += sk[k] ? si[k] >> 27 : 0u;  // kept leaves' triangle counts
     }
@@ -1693,13 +1692,16 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
   // let the compiler thread lanes 1-63 straight back to the body past the head, where they spun on
   // a stale item: keep it this way.
   Coop solo{0u, 1u, nullptr, 0u, 0u};
-  uint32_t prev_tile = 0xFFFFFFFFu, prev_cost = 0;
+  uint32_t prev_tile = 0xFFFFFFFFu, prev_cost = 0, prev_lk = 0;
   for (;;) {
     uint32_t t = 0;
     if (lane == 0) {
       if (prev_tile != 0xFFFFFFFFu) {
+        // a tile's cost: its items' summed clocks; the heavy threshold's sum counts an item by its
+        // share of the tile's lanes (its work), so splitting does not raise the threshold (with summed
+        // clocks there too, borderline tiles flipped between split and whole: 7.4 / 8.4 ms frames)
         atomicAdd(&P.tile_cost[prev_tile], prev_cost);
-        atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)prev_cost);
+        atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)(prev_cost >> prev_lk));
       }
       t = first + atomicAdd(&P.sched[0], 1u);
     }
@@ -1721,10 +1723,11 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     const uint64_t c = CoopOk ? (uint64_t)solo.work : (__builtin_readcyclecounter() - t0) >> 4;
     prev_cost = __builtin_amdgcn_readfirstlane(c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c);
     prev_tile = tile;
+    prev_lk = lk;
   }
   if (lane == 0 && prev_tile != 0xFFFFFFFFu) {
     atomicAdd(&P.tile_cost[prev_tile], prev_cost);
-    atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)prev_cost);
+    atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)(prev_cost >> prev_lk));
   }
 }
 
@@ -2047,6 +2050,8 @@ int resolve_variant(const TraceParams& p, int variant) {
   return variant;
 }
 
+static uint32_t tiles_of(const TraceParams& p) { return ((p.pc.width + 7) / 8) * ((p.local_rows + 7) / 8); }
+
 // Persistent kernels: plan this trace from the last one's tile costs (when p.plan_valid and
 // splitting is on), then reset the counters the trace fills.  q.items = nullptr: plain tile order.
 static hipError_t prepare_schedule(TraceParams& q, hipStream_t stream) {
@@ -2121,10 +2126,12 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       TraceParams q = p;
       q.coop = 0;
-      // auto: a pair step's work scales with the rays in the batch, so heavy tiles (> 2x a resident
-      // wave's fair share) run as 2, 4 or 8 row groups by cost (profiles/r01n_wq_plan_sweep.jsonl)
+      // auto: a pair step's work scales with the rays in the batch, so heavy tiles (> factor x a
+      // resident wave's fair share of the work) run as 2, 4 or 8 items by cost; factor 2 when a
+      // resident wave gets more than 6 tiles (the full frame), else 3 (row partitions at N > 1)
+      // (profiles/r01o_lane_weighted_sum_factor_sweep.jsonl)
       if (q.split_k == 0) q.split_k = 8;
-      if (q.split_factor < 0) q.split_factor = 2;
+      if (q.split_factor < 0) q.split_factor = tiles_of(p) > 6 * p.num_cus * 16u ? 2 : 3;
       const size_t lds = wq_lds_bytes(p, &q.wq_ncap, &q.wq_tcap);
       if (p.wq_ncap) q.wq_ncap = std::min(q.wq_ncap, std::max(128u, p.wq_ncap & ~63u));  // HRT_OPT_WQ_NODE_CAP
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;

@@ -240,9 +240,10 @@ def test_leaf_sizes(leaf):
 
 @pytest.mark.parametrize("scene", ["island", "cave", "box"])
 def test_wq_node_image(scene):
-    """BUNDLE_WQ's 48 B node image (hrt_bvh.h make_wq_nodes) against the full nodes: boxes, margins,
-    leaf info / right child and escape copied exactly; the binary16 cone only ever widens (cos
-    rounded down, sin up) and the axis is within 2^-12 per component (kernel allows 5e-4 in d.axis)."""
+    """BUNDLE_WQ's 48 B node image (hrt_bvh.h make_wq_nodes) against the full preorder nodes: the same
+    boxes and margins in sibling-adjacent order (an inner node's children at fc, fc + 1), leaf info
+    copied, escapes that continue a stackless walk after each subtree; the binary16 cone only ever
+    widens (cos rounded down, sin up) and the axis is within 2^-12 per component (kernel: 5e-4)."""
     case = SceneCase(scene, (8, 8), 1, 1)
     b = build(case.tris, case.meshes, 4)
     if b is None:
@@ -254,16 +255,40 @@ def test_wq_node_image(scene):
                                      len(case.meshes), 4, img.ctypes.data, img.size)
     assert got == nn
     img = img.reshape(nn, 12)
-    N = b["nodes"]
-    np.testing.assert_array_equal(bits(img[:, 0:8]), bits(N[:, 0:8]))
     w = bits(img[:, 8:12])
-    np.testing.assert_array_equal(w[:, 3], bits(N[:, 14]))                 # leaf info / right child
-    np.testing.assert_array_equal(w[:, 2] >> 16, bits(N[:, 15]))           # escape
+    N = b["nodes"]
+    Nu = N.view(np.uint32)
+    # map preorder node -> image node by walking both trees together
+    new_of = np.full(nn, -1, np.int64)
+    esc_of = np.full(nn, -1, np.int64)
+    new_of[0], esc_of[0] = 0, nn
+    for k in range(nn):
+        info = int(Nu[k, 14])
+        if info >> 27:
+            continue
+        fc = int(w[new_of[k], 3])
+        left, right = k + 1, info
+        new_of[left], new_of[right] = fc, fc + 1
+        esc_of[left], esc_of[right] = fc + 1, esc_of[k]
+    assert sorted(new_of.tolist()) == list(range(nn))
+    img_o = img[new_of]
+    w_o = w[new_of]
+    np.testing.assert_array_equal(bits(img_o[:, 0:8]), bits(N[:, 0:8]))
+    leaf = (Nu[:, 14] >> 27) > 0
+    np.testing.assert_array_equal(w_o[leaf, 3], Nu[leaf, 14])          # leaf info
+    np.testing.assert_array_equal(w_o[:, 2] >> 16, esc_of)              # escapes
     half = lambda u: (u & 0xFFFF).astype(np.uint16).view(np.float16).astype(np.float64)
-    ax, ay, az = half(w[:, 0]), half(w[:, 0] >> 16), half(w[:, 1])
-    cq, sq = half(w[:, 1] >> 16), half(w[:, 2])
+    ax, ay, az = half(w_o[:, 0]), half(w_o[:, 0] >> 16), half(w_o[:, 1])
+    cq, sq = half(w_o[:, 1] >> 16), half(w_o[:, 2])
     axis = N[:, 8:11].astype(np.float64)
     assert np.abs(np.stack([ax, ay, az], 1) - axis).max() <= 2.0 ** -12
     assert (cq <= N[:, 11].astype(np.float64)).all() and (cq >= 0).all()
     assert (sq >= N[:, 12].astype(np.float64)).all()
     assert np.linalg.norm(np.stack([ax, ay, az], 1) - axis, axis=1).max() <= 5e-4  # |d.(A16 - A)| <= |A16 - A|
+    # a stackless walk over the image visits every node once, in preorder of the full tree
+    order, cur = [], 0
+    while cur != nn:
+        order.append(cur)
+        info = int(w[cur, 3])
+        cur = info if not (info >> 27) else int(w[cur, 2] >> 16)
+    assert order == new_of.tolist()
