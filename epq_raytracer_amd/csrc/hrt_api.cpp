@@ -81,7 +81,7 @@ struct hrt_context {
   uint32_t* bvh_band_off = nullptr;
   uint32_t* bvh_entries = nullptr;
   uint32_t* bvh_keybase = nullptr;
-  float4* bvh_band = nullptr;
+  uint2* bvh_band = nullptr;       // grazing-band entries, 8 B (hrt_bvh.h kBand*)
   uint32_t bvh_info[HRT_NUM_SCENE_INFO] = {};  // hrt_get_scene_info
   float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f;
   uint32_t bvh_leaf = 4;
@@ -360,7 +360,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
     if ((st = up(ctx->bvh_prims, bvh.prims)) != HRT_OK) return st;
     if ((st = up(ctx->bvh_irregular, bvh.irregular)) != HRT_OK) return st;
     if ((st = up(ctx->bvh_band_off, bvh.band_off)) != HRT_OK) return st;
-    if ((st = up(ctx->bvh_band, bvh.band_list)) != HRT_OK) return st;  // 16 B entries
+    if ((st = up(ctx->bvh_band, bvh.band_list)) != HRT_OK) return st;  // 8 B entries
     if ((st = up(ctx->bvh_entries, bvh.entries)) != HRT_OK) return st;
     if ((st = up(ctx->bvh_keybase, bvh.key_base)) != HRT_OK) return st;
   }
@@ -372,7 +372,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   ctx->bvh_abs_coef = bvh.abs_coef;
   ctx->bvh_built_leaf = std::max(1u, std::min(ctx->bvh_leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
   ctx->bvh_rel_t = bvh.rel_t;
-  ctx->bvh_info[5] = (uint32_t)(bvh.band_list.size() / 4);
+  ctx->bvh_info[5] = (uint32_t)(bvh.band_list.size() / 2);
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
   if (!keep_rays) ctx->n_rays = n_rays;
   ctx->plan_valid = false;  // tile costs describe the old scene

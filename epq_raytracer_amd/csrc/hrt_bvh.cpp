@@ -295,16 +295,17 @@ void build_band_lists(BvhHost& out) {
   worker();
   for (auto& th : pool) th.join();
   for (int c = 0; c < kDirCells; ++c) out.band_off[c + 1] = out.band_off[c] + (uint32_t)lists[c].size();
-  out.band_list.reserve((size_t)out.band_off[kDirCells] * 4);
+  out.band_list.reserve((size_t)out.band_off[kDirCells] * 2);
   for (int c = 0; c < kDirCells; ++c) {
     for (uint32_t k : lists[c]) {
-      // (n / |n|, prim index bits): the kernel's pre-check of d.n^ against the band
+      // 8 B: the prim index and n / |n| in fixed point (hrt_bvh.h kBand*): the kernel's pre-check of
+      // d.n^ against the band, widened by the quantization error
       const float* n = &out.prims[(size_t)k * 16 + 12];
       const double inv = 1.0 / norm(ld(n));
-      const float e[4] = {(float)(n[0] * inv), (float)(n[1] * inv), (float)(n[2] * inv), bits_f(k)};
-      uint32_t w[4];
-      std::memcpy(w, e, 16);
-      out.band_list.insert(out.band_list.end(), w, w + 4);
+      const int32_t qx = (int32_t)std::lround(n[0] * inv * kBandQx), qy = (int32_t)std::lround(n[1] * inv * kBandQyz),
+                    qz = (int32_t)std::lround(n[2] * inv * kBandQyz);
+      out.band_list.push_back(k | ((uint32_t)qx & 0x3FFFu) << 18);
+      out.band_list.push_back(((uint32_t)qy & 0xFFFFu) | ((uint32_t)qz & 0xFFFFu) << 16);
     }
   }
 }
@@ -463,7 +464,7 @@ extern "C" int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, co
   counts[2] = b.n_irregular;
   counts[3] = b.n_never;
   counts[4] = built ? 1u : 0u;
-  counts[5] = (uint32_t)(b.band_list.size() / 4);
+  counts[5] = (uint32_t)(b.band_list.size() / 2);
   if (!built) return 0;
   auto copy = [](auto* dst, uint64_t cap, const auto& v) {
     if (dst && cap >= v.size()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));

@@ -39,7 +39,7 @@ struct BvhHost {
   std::vector<uint32_t> entries;    // per leaf prim: triangle index | mesh << 26
   std::vector<uint32_t> key_base;   // per mesh: scan key of (m, i) = key_base[m] + i (mod 2^32)
   std::vector<uint32_t> band_off;   // 6 kDirRes^2 + 1 offsets into band_list
-  std::vector<uint32_t> band_list;  // 4 words per entry: n^ (3 floats, rounded), prim index
+  std::vector<uint32_t> band_list;  // 2 words per entry: prim | n^x << 18, n^y | n^z << 16 (kBand*)
   std::vector<float> wq_nodes;      // BUNDLE_WQ's 48 B node image (make_wq_nodes)
   bool wq_ok = false;               // the image exists (at most 65535 nodes)
   uint32_t n_nodes = 0, n_prims = 0, n_irregular = 0, n_never = 0;  // never = zero normal (dn == 0)
@@ -48,6 +48,12 @@ struct BvhHost {
 };
 
 constexpr float kBandTau = 3e-3f;
+// Grazing-band entries (8 B): prim index (18 bits, kBvhMaxEntries) | round(n^x * kBandQx) as a signed
+// 14-bit field << 18; round(n^y * kBandQyz) | round(n^z * kBandQyz) << 16, signed 16-bit fields.
+// |n^ - decoded| <= 0.5 / kBandQx in x, 0.5 / kBandQyz in y, z: |d.n^ - d.decoded| <= 6.2e-5 for |d| = 1,
+// and the kernels widen their pre-check window by kBandQErr.
+constexpr float kBandQx = 8191.0f, kBandQyz = 32767.0f;
+constexpr float kBandQErr = 7e-5f;
 constexpr int kDirRes = 128;
 constexpr int kDirCells = 6 * kDirRes * kDirRes;
 

@@ -50,7 +50,7 @@ struct TraceParams {
   const float4* bvh_prims;       // 4 float4 per leaf triangle
   const float4* bvh_irregular;   // 4 float4 per entry outside the analysis (tested for every ray)
   const uint32_t* bvh_band_off;  // kDirCells + 1 offsets: grazing-band prims per direction cell
-  const float4* bvh_band;        // (n^, prim index bits) per entry
+  const uint2* bvh_band;         // 8 B per entry (hrt_bvh.h kBand*): prim index, quantized n^
   const uint32_t* bvh_entries;   // per leaf prim: triangle index | mesh << 26 (BUNDLE_BVH_LDS)
   const uint32_t* bvh_keybase;   // per mesh: key = keybase[m] + triangle index
   uint32_t bvh_n_nodes, bvh_n_irregular, bvh_n_prims, bvh_n_meshes;

@@ -1013,6 +1013,22 @@ __device__ __forceinline__ uint32_t dir_cell(f3 d) {
   return (face * kDirRes + (uint32_t)iu) * kDirRes + (uint32_t)iv;
 }
 
+// Grazing-band pre-check (hrt_bvh.h kBand*): d.n^ of an 8 B entry, with d pre-scaled by the fixed-point
+// steps (ds = d / (kBandQx, kBandQyz, kBandQyz)); the window is widened by kBandQErr.
+struct BandCheck {
+  f3 ds;
+  float lo, hi;
+  __device__ __forceinline__ explicit BandCheck(f3 d, float lo0, float hi0)
+      : ds(mk(d.x / kBandQx, d.y / kBandQyz, d.z / kBandQyz)), lo(lo0 - kBandQErr), hi(hi0 + kBandQErr) {}
+  __device__ __forceinline__ bool in(uint2 e) const {
+    const float qx = (float)__builtin_amdgcn_sbfe((int)e.x, 18, 14);
+    const float qy = (float)__builtin_amdgcn_sbfe((int)e.y, 0, 16), qz = (float)__builtin_amdgcn_sbfe((int)e.y, 16, 16);
+    const float dn = ds.x * qx + ds.y * qy + ds.z * qz;
+    return dn > lo && dn < hi;
+  }
+  __device__ __forceinline__ static uint32_t prim(uint2 e) { return e.x & 0x3FFFFu; }
+};
+
 // Bounce segments through the hierarchy.  Called with ALL 64 lanes active (spheres and the
 // irregular list are wave-uniform loops; the traversal and the band list are per lane).
 template <bool D, class Bvh>
@@ -1050,27 +1066,24 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
   if (sec && mask) {
     const uint32_t cell = dir_cell(d);
     const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
-    // Pre-check: the stored n^ is within 1e-7 of n / |n| per component, so |d.n^stored - d.n^| < 1e-6
-    // and an entry outside (-kBandTau - 2e-5, 3e-5) is not in this lane's band.
-    const float lo = -kBandTau - 2e-5f, hi = 3e-5f;
+    // Pre-check: an entry whose decoded d.n^ is outside (-kBandTau - 2e-5, 3e-5) widened by the
+    // quantization error is not in this lane's band (-kBandTau - 1e-5, 2e-5).
+    const BandCheck bc(d, -kBandTau - 2e-5f, 3e-5f);
     uint32_t k = b0;
     for (; k + 4 <= b1; k += 4) {
-      const float4 q0 = P.bvh_band[k], q1 = P.bvh_band[k + 1], q2 = P.bvh_band[k + 2], q3 = P.bvh_band[k + 3];
-      const float4 qs[4] = {q0, q1, q2, q3};
+      const uint2 qs[4] = {P.bvh_band[k], P.bvh_band[k + 1], P.bvh_band[k + 2], P.bvh_band[k + 3]};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float dn = d.x * qs[j].x + d.y * qs[j].y + d.z * qs[j].z;
-        if (dn > lo && dn < hi) {
-          bvh.prim(__builtin_bit_cast(uint32_t, qs[j].w), mask, o, d, c, bkey, best_k);
+        if (bc.in(qs[j])) {
+          bvh.prim(BandCheck::prim(qs[j]), mask, o, d, c, bkey, best_k);
           ++band_tests;
         }
       }
     }
     for (; k < b1; ++k) {
-      const float4 q = P.bvh_band[k];
-      const float dn = d.x * q.x + d.y * q.y + d.z * q.z;
-      if (dn > lo && dn < hi) {
-        bvh.prim(__builtin_bit_cast(uint32_t, q.w), mask, o, d, c, bkey, best_k);
+      const uint2 q = P.bvh_band[k];
+      if (bc.in(q)) {
+        bvh.prim(BandCheck::prim(q), mask, o, d, c, bkey, best_k);
         ++band_tests;
       }
     }
@@ -1262,24 +1275,22 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #endif
     const uint32_t cell = dir_cell(d);
     const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
-    const float lo = -kBandTau - 2e-5f, hi = 3e-5f;  // see world_hit_bounce_bvh
+    const BandCheck bc(d, -kBandTau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
     uint32_t k = b0;
     for (; k + 4 <= b1; k += 4) {
-      const float4 qs[4] = {P.bvh_band[k], P.bvh_band[k + 1], P.bvh_band[k + 2], P.bvh_band[k + 3]};
+      const uint2 qs[4] = {P.bvh_band[k], P.bvh_band[k + 1], P.bvh_band[k + 2], P.bvh_band[k + 3]};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float dn = d.x * qs[j].x + d.y * qs[j].y + d.z * qs[j].z;
-        if (dn > lo && dn < hi) {
-          g.prim(__builtin_bit_cast(uint32_t, qs[j].w), mask, o, d, c, bkey, best_k);
+        if (bc.in(qs[j])) {
+          g.prim(BandCheck::prim(qs[j]), mask, o, d, c, bkey, best_k);
           ++band_tests;
         }
       }
     }
     for (; k < b1; ++k) {
-      const float4 q = P.bvh_band[k];
-      const float dn = d.x * q.x + d.y * q.y + d.z * q.z;
-      if (dn > lo && dn < hi) {
-        g.prim(__builtin_bit_cast(uint32_t, q.w), mask, o, d, c, bkey, best_k);
+      const uint2 q = P.bvh_band[k];
+      if (bc.in(q)) {
+        g.prim(BandCheck::prim(q), mask, o, d, c, bkey, best_k);
         ++band_tests;
       }
     }

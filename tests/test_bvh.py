@@ -35,7 +35,7 @@ def build(tris, meshes, leaf=4):
     prims = np.zeros(max(npr, 1) * 16, np.float32)
     irr = np.zeros(max(nirr, 1) * 16, np.float32)
     boff = np.zeros(CELLS + 1, np.uint32)
-    band = np.zeros(max(nband, 1) * 4, np.uint32)
+    band = np.zeros(max(nband, 1) * 2, np.uint32)
     r = lib.hrt_debug_bvh_build(tris.ctypes.data, len(tris), meshes.ctypes.data, len(meshes), leaf, counts,
                                 P(nodes.ctypes.data), nodes.size, P(prims.ctypes.data), prims.size,
                                 P(irr.ctypes.data), irr.size, P(boff.ctypes.data), boff.size,
@@ -43,7 +43,7 @@ def build(tris, meshes, leaf=4):
     assert r == 1
     return dict(nodes=nodes[:nn * 16].reshape(nn, 16), prims=prims[:npr * 16].reshape(npr, 16),
                 irregular=irr[:nirr * 16].reshape(nirr, 16), never=nnever, band_off=boff,
-                band=band[:nband * 4].reshape(nband, 4))
+                band=band[:nband * 2].reshape(nband, 2))
 
 
 def bits(a):
@@ -195,7 +195,7 @@ def test_band_lists_cover_every_grazing_triangle(built):
     d = np.concatenate([d, edge, inplane])
     d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
     cells = dir_cell(d)
-    band_idx = b["band"][:, 3]
+    band_idx = b["band"][:, 0] & 0x3FFFF
     off = b["band_off"]
     lo, hi = -(float(TAU_G) + 1e-5), 2e-5
     for i in range(len(d)):
@@ -209,16 +209,28 @@ def test_band_lists_cover_every_grazing_triangle(built):
         assert not missing, f"direction {d[i]} cell {c}: band prims {missing[:5]} missing"
 
 
+def decode_band(band):
+    """8 B band entries (hrt_bvh.h kBand*): prim index, n^ decoded from its fixed-point fields."""
+    w0, w1 = band[:, 0].astype(np.uint32), band[:, 1].astype(np.uint32)
+    qx = (w0 >> 18).astype(np.int32)
+    qx = np.where(qx >= 1 << 13, qx - (1 << 14), qx)
+    qy = (w1 & 0xFFFF).astype(np.uint16).view(np.int16).astype(np.float64)
+    qz = (w1 >> 16).astype(np.uint16).view(np.int16).astype(np.float64)
+    return w0 & 0x3FFFF, np.stack([qx / 8191.0, qy / 32767.0, qz / 32767.0], 1)
+
+
 def test_band_entries_are_unit_normals_of_their_prims(built):
+    """Each entry's fixed-point n^ is within half a step of its prim's unit normal, so |d.n^ - d.decoded|
+    <= 6.5e-5 < kBandQErr (7e-5) for unit d."""
     case, b = built
     if len(b["band"]) == 0:
         return
-    band = b["band"]
-    k = band[:, 3]
+    k, stored = decode_band(b["band"])
     n = b["prims"][k, 12:15].astype(np.float64)
     nh = n / np.linalg.norm(n, axis=1, keepdims=True)
-    stored = band[:, :3].view(np.float32).astype(np.float64)
-    assert np.abs(stored - nh).max() < 2e-7
+    err = np.abs(stored - nh)
+    assert err[:, 0].max() <= 0.5 / 8191 + 1e-9 and err[:, 1:].max() <= 0.5 / 32767 + 1e-9
+    assert np.linalg.norm(stored - nh, axis=1).max() < 7e-5
 
 
 def test_not_built_above_the_mesh_limit():
