@@ -85,7 +85,8 @@ struct hrt_context {
   uint32_t bvh_info[HRT_NUM_SCENE_INFO] = {};  // hrt_get_scene_info
   float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f;
   uint32_t bvh_leaf = 4;
-  uint32_t bvh_built_leaf = 4;  // leaf size of the hierarchy the last hrt_set_scene built
+  uint32_t bvh_built_leaf = 4;   // leaf size of the hierarchy the last hrt_set_scene built
+  uint32_t bvh_dir_res = 64;     // direction cells per face edge of its band lists
 
   int variant = 0;
   bool counters_on = true;
@@ -370,6 +371,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   ctx->bvh_info[3] = bvh.n_never;
   ctx->bvh_info[4] = built ? 1u : 0u;
   ctx->bvh_abs_coef = bvh.abs_coef;
+  ctx->bvh_dir_res = bvh.dir_res;
   ctx->bvh_built_leaf = std::max(1u, std::min(ctx->bvh_leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
   ctx->bvh_rel_t = bvh.rel_t;
   ctx->bvh_info[5] = (uint32_t)(bvh.band_list.size() / 2);
@@ -439,6 +441,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.bvh_prims = ctx->bvh_prims;
   p.bvh_irregular = ctx->bvh_irregular;
   p.bvh_band_off = ctx->bvh_band_off;
+  p.bvh_dir_res = ctx->bvh_dir_res;
   p.bvh_band = ctx->bvh_band;
   p.bvh_entries = ctx->bvh_entries;
   p.bvh_keybase = ctx->bvh_keybase;

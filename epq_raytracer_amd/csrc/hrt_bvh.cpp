@@ -262,7 +262,9 @@ void build_band_lists(BvhHost& out) {
     const V3 n = ld(&out.prims[(size_t)k * 16 + 12]);
     nh[k] = n * (1.0 / norm(n));
   }
-  constexpr int kCoarse = 8, kSub = kDirRes / kCoarse;
+  const int kDirRes = (int)out.dir_res, kDirCells = 6 * kDirRes * kDirRes;
+  constexpr int kCoarse = 8;
+  const int kSub = kDirRes / kCoarse;
   out.band_off.assign(kDirCells + 1, 0);
   std::vector<std::vector<uint32_t>> lists(kDirCells);
   // one task per coarse cell: its candidates, then its kSub x kSub fine cells
@@ -440,6 +442,7 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
     Builder bld{entries, leaf_size, out};
     bld.build(0, (uint32_t)entries.size(), tris);
   }
+  out.dir_res = (uint32_t)dir_res_for(out.n_prims);
   build_band_lists(out);
   // t-slack of the box test for a lane at distance <= R: abs = abs_coef R, rel
   const double e = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)kBandTau - out.rho_max - 4e-7);
@@ -453,7 +456,7 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
 
 // ---- host-only inspection (tests/test_bvh.py): build and copy out, no GPU involved ----------------
 extern "C" int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes,
-                                   uint32_t n_meshes, uint32_t leaf_size, uint32_t counts[6], float* nodes,
+                                   uint32_t n_meshes, uint32_t leaf_size, uint32_t counts[7], float* nodes,
                                    uint64_t nodes_cap, float* prims, uint64_t prims_cap, float* irregular,
                                    uint64_t irregular_cap, uint32_t* band_off, uint64_t band_off_cap,
                                    uint32_t* band_list, uint64_t band_list_cap) {
@@ -465,6 +468,7 @@ extern "C" int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, co
   counts[3] = b.n_never;
   counts[4] = built ? 1u : 0u;
   counts[5] = (uint32_t)(b.band_list.size() / 2);
+  counts[6] = b.dir_res;
   if (!built) return 0;
   auto copy = [](auto* dst, uint64_t cap, const auto& v) {
     if (dst && cap >= v.size()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));

@@ -30,7 +30,7 @@ namespace hrt {
 //
 // Grazing band: the box cull's error bound needs |d.n^| >= kBandTau for front-facing triangles, so
 // every triangle with d.n^ in (-kBandTau, +2e-5) ("in the band" of d) is tested separately.  Ray
-// directions are binned on a cube map (face, iu, iv), kDirRes x kDirRes cells per face; band_list of a
+// directions are binned on a cube map (face, iu, iv), dir_res x dir_res cells per face; band_list of a
 // cell holds every leaf prim that is in the band of SOME direction of that cell.
 struct BvhHost {
   std::vector<float> nodes;
@@ -38,7 +38,8 @@ struct BvhHost {
   std::vector<float> irregular;  // entries the analysis does not cover: tested for every bounce ray
   std::vector<uint32_t> entries;    // per leaf prim: triangle index | mesh << 26
   std::vector<uint32_t> key_base;   // per mesh: scan key of (m, i) = key_base[m] + i (mod 2^32)
-  std::vector<uint32_t> band_off;   // 6 kDirRes^2 + 1 offsets into band_list
+  std::vector<uint32_t> band_off;   // 6 dir_res^2 + 1 offsets into band_list
+  uint32_t dir_res = 64;            // direction cells per face edge (dir_res_for)
   std::vector<uint32_t> band_list;  // 2 words per entry: prim | n^x << 18, n^y | n^z << 16 (kBand*)
   std::vector<float> wq_nodes;      // BUNDLE_WQ's 48 B node image (make_wq_nodes)
   bool wq_ok = false;               // the image exists (at most 65535 nodes)
@@ -54,8 +55,12 @@ constexpr float kBandTau = 3e-3f;
 // and the kernels widen their pre-check window by kBandQErr.
 constexpr float kBandQx = 8191.0f, kBandQyz = 32767.0f;
 constexpr float kBandQErr = 7e-5f;
-constexpr int kDirRes = 128;
-constexpr int kDirCells = 6 * kDirRes * kDirRes;
+// Direction cells per cube-map face edge: finer cells mean shorter per-ray lists (a ray scans its
+// cell's list on every bounce) but ~linearly more entries per triangle (a triangle's band is a
+// great-circle strip).  256 up to 8K entries (island: 9 entries per list, 29 MB), 128 up to 32K, 64
+// above (profiles/r01p_*).
+constexpr int kDirResMax = 256;
+inline int dir_res_for(uint64_t entries) { return entries <= 8192 ? 256 : entries <= 32768 ? 128 : 64; }
 
 constexpr uint32_t kBvhMaxMeshes = 64;     // per-lane mesh filter is a 64-bit mask
 constexpr uint32_t kBvhMaxLeafCount = 16;  // leaf count lives in bits 27..31 of node word 14

@@ -49,7 +49,8 @@ struct TraceParams {
   const float4* bvh_wq_nodes;    // 3 float4 per node: BUNDLE_WQ's image (hrt_bvh.h make_wq_nodes), or nullptr
   const float4* bvh_prims;       // 4 float4 per leaf triangle
   const float4* bvh_irregular;   // 4 float4 per entry outside the analysis (tested for every ray)
-  const uint32_t* bvh_band_off;  // kDirCells + 1 offsets: grazing-band prims per direction cell
+  const uint32_t* bvh_band_off;  // 6 bvh_dir_res^2 + 1 offsets: grazing-band prims per direction cell
+  uint32_t bvh_dir_res;          // direction cells per cube-map face edge
   const uint2* bvh_band;         // 8 B per entry (hrt_bvh.h kBand*): prim index, quantized n^
   const uint32_t* bvh_entries;   // per leaf prim: triangle index | mesh << 26 (BUNDLE_BVH_LDS)
   const uint32_t* bvh_keybase;   // per mesh: key = keybase[m] + triangle index

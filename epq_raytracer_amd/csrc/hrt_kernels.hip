@@ -990,7 +990,7 @@ __device__ __forceinline__ bool bvh_node_visit(const float4& N0, const float4& N
 }
 // Cube-map cell of a direction (hrt_bvh.cpp face_dir is the inverse): face = 2 * major axis +
 // (component < 0), (u, v) = the two minor components over the major one's magnitude.
-__device__ __forceinline__ uint32_t dir_cell(f3 d) {
+__device__ __forceinline__ uint32_t dir_cell(f3 d, uint32_t res) {
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
   uint32_t face;
   float u, v;
@@ -1007,10 +1007,10 @@ __device__ __forceinline__ uint32_t dir_cell(f3 d) {
     u = d.x / az;
     v = d.y / az;
   }
-  const float s = 0.5f * (float)kDirRes;
-  const int iu = min(kDirRes - 1, max(0, (int)((u + 1.0f) * s)));  // NaN converts to 0
-  const int iv = min(kDirRes - 1, max(0, (int)((v + 1.0f) * s)));
-  return (face * kDirRes + (uint32_t)iu) * kDirRes + (uint32_t)iv;
+  const float s = 0.5f * (float)res;
+  const int iu = min((int)res - 1, max(0, (int)((u + 1.0f) * s)));  // NaN converts to 0
+  const int iv = min((int)res - 1, max(0, (int)((v + 1.0f) * s)));
+  return (face * res + (uint32_t)iu) * res + (uint32_t)iv;
 }
 
 // Grazing-band pre-check (hrt_bvh.h kBand*): d.n^ of an 8 B entry, with d pre-scaled by the fixed-point
@@ -1064,7 +1064,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
   uint32_t node = (sec && mask) ? 0u : end;
   uint32_t visits = 0, prim_tests = 0, band_tests = 0;
   if (sec && mask) {
-    const uint32_t cell = dir_cell(d);
+    const uint32_t cell = dir_cell(d, P.bvh_dir_res);
     const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
     // Pre-check: an entry whose decoded d.n^ is outside (-kBandTau - 2e-5, 3e-5) widened by the
     // quantization error is not in this lane's band (-kBandTau - 1e-5, 2e-5).
@@ -1273,7 +1273,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #else
   if (sec && mask) {
 #endif
-    const uint32_t cell = dir_cell(d);
+    const uint32_t cell = dir_cell(d, P.bvh_dir_res);
     const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
     const BandCheck bc(d, -kBandTau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
     uint32_t k = b0;

@@ -36,12 +36,12 @@ uint32_t hrt_host_ray_grid(uint32_t width, uint32_t height, float camera_focal_l
                            const float up[3], float first[3], float px[3], float py[3], float* default_jitter);
 
 /* Host-only inspection of the hierarchy hrt_set_scene builds for BUNDLE_BVH (tests; no GPU).
- * counts = {nodes, prims, irregular, never, built, band entries}; each array (capacity in elements:
- * floats for nodes/prims/irregular = 16 per record, u32 for band_off = 6*128*128+1 and band_list =
- * 2 per entry) is filled when non-NULL and large enough.  Returns 1 (filled), 0 (not built),
- * -1 (a capacity too small). */
+ * counts = {nodes, prims, irregular, never, built, band entries, direction cells per face edge R};
+ * each array (capacity in elements: floats for nodes/prims/irregular = 16 per record, u32 for
+ * band_off = 6*R*R+1 (R <= 256) and band_list = 2 per entry) is filled when non-NULL and large
+ * enough.  Returns 1 (filled), 0 (not built), -1 (a capacity too small). */
 int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
-                        uint32_t leaf_size, uint32_t counts[6], float* nodes, uint64_t nodes_cap, float* prims,
+                        uint32_t leaf_size, uint32_t counts[7], float* nodes, uint64_t nodes_cap, float* prims,
                         uint64_t prims_cap, float* irregular, uint64_t irregular_cap, uint32_t* band_off,
                         uint64_t band_off_cap, uint32_t* band_list, uint64_t band_list_cap);
 

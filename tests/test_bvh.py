@@ -18,23 +18,22 @@ import pytest
 from helpers import E, SceneCase, _lib
 
 TAU_G = np.float32(3e-3)   # hrt_bvh.h kBandTau
-DIR_RES = 128              # hrt_bvh.h kDirRes
-CELLS = 6 * DIR_RES * DIR_RES
+DIR_RES_MAX = 256          # hrt_bvh.h kDirResMax (the scene's resolution comes back in counts[6])
 
 
 def build(tris, meshes, leaf=4):
     lib = _lib.load()
-    counts = (ctypes.c_uint32 * 6)()
+    counts = (ctypes.c_uint32 * 7)()
     P = ctypes.c_void_p
     r = lib.hrt_debug_bvh_build(tris.ctypes.data, len(tris), meshes.ctypes.data, len(meshes), leaf, counts,
                                 None, 0, None, 0, None, 0, None, 0, None, 0)
-    nn, npr, nirr, nnever, built, nband = list(counts)
+    nn, npr, nirr, nnever, built, nband, res = list(counts)
     if not built:
         return None
     nodes = np.zeros(max(nn, 1) * 16, np.float32)
     prims = np.zeros(max(npr, 1) * 16, np.float32)
     irr = np.zeros(max(nirr, 1) * 16, np.float32)
-    boff = np.zeros(CELLS + 1, np.uint32)
+    boff = np.zeros(6 * res * res + 1, np.uint32)
     band = np.zeros(max(nband, 1) * 2, np.uint32)
     r = lib.hrt_debug_bvh_build(tris.ctypes.data, len(tris), meshes.ctypes.data, len(meshes), leaf, counts,
                                 P(nodes.ctypes.data), nodes.size, P(prims.ctypes.data), prims.size,
@@ -42,7 +41,7 @@ def build(tris, meshes, leaf=4):
                                 P(band.ctypes.data), band.size)
     assert r == 1
     return dict(nodes=nodes[:nn * 16].reshape(nn, 16), prims=prims[:npr * 16].reshape(npr, 16),
-                irregular=irr[:nirr * 16].reshape(nirr, 16), never=nnever, band_off=boff,
+                irregular=irr[:nirr * 16].reshape(nirr, 16), never=nnever, band_off=boff, dir_res=res,
                 band=band[:nband * 2].reshape(nband, 2))
 
 
@@ -162,7 +161,7 @@ def test_tree_structure_boxes_and_cones(built):
     assert (covered == 1).all()
 
 
-def dir_cell(d):
+def dir_cell(d, res):
     """The kernel's dir_cell in binary32 (hrt_kernels.hip)."""
     d = d.astype(np.float32)
     a = np.abs(d)
@@ -173,10 +172,10 @@ def dir_cell(d):
     with np.errstate(divide="ignore", invalid="ignore"):
         u = np.where(fx, d[:, 1] / a[:, 0], np.where(fy, d[:, 2] / a[:, 1], d[:, 0] / a[:, 2])).astype(np.float32)
         v = np.where(fx, d[:, 2] / a[:, 0], np.where(fy, d[:, 0] / a[:, 1], d[:, 1] / a[:, 2])).astype(np.float32)
-    s = np.float32(0.5 * DIR_RES)
-    iu = np.clip(((u + np.float32(1)) * s).astype(np.int64), 0, DIR_RES - 1)
-    iv = np.clip(((v + np.float32(1)) * s).astype(np.int64), 0, DIR_RES - 1)
-    return (face * DIR_RES + iu) * DIR_RES + iv
+    s = np.float32(0.5 * res)
+    iu = np.clip(((u + np.float32(1)) * s).astype(np.int64), 0, res - 1)
+    iv = np.clip(((v + np.float32(1)) * s).astype(np.int64), 0, res - 1)
+    return (face * res + iu) * res + iv
 
 
 def test_band_lists_cover_every_grazing_triangle(built):
@@ -194,7 +193,7 @@ def test_band_lists_cover_every_grazing_triangle(built):
     inplane = np.cross(nh[t], rng.normal(size=(300, 3)))
     d = np.concatenate([d, edge, inplane])
     d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
-    cells = dir_cell(d)
+    cells = dir_cell(d, b["dir_res"])
     band_idx = b["band"][:, 0] & 0x3FFFF
     off = b["band_off"]
     lo, hi = -(float(TAU_G) + 1e-5), 2e-5
