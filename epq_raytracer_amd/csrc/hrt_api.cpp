@@ -475,6 +475,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
     q.counters = nullptr;
     q.diag = nullptr;
     q.tile_cycles = nullptr;
+    q.probe = 1u;
     int ran = 0, blk = 0;
     if (hipError_t pe = hrt::launch_trace(q, variant, ctx->stream, &ran, &blk); pe != hipSuccess)
       return hip_fail(ctx, pe, "probe trace launch");

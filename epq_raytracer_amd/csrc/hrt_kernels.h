@@ -43,6 +43,9 @@ struct TraceParams {
   uint32_t split_prio;           // heavy items run at raised wave priority (s_setprio 3)
   uint32_t coop;                 // heavy tiles run cooperatively by a whole workgroup (BUNDLE_CULL_LDS)
   uint32_t plan_valid;           // tile_cost holds the previous trace's costs of this context
+  uint32_t probe;                // a 1-sample planning probe (HRT_OPT_PROBE): launched as the diagnostics
+                                 // instantiation (<.., true>, all diagnostics pointers null) so that
+                                 // profilers list it apart from the frame's trace kernel
   uint32_t num_cus;              // compute units of the device (persistent grid size)
   // BUNDLE_BVH: bounce-segment hierarchy built by hrt_set_scene (hrt_bvh.h records); nullptr = none.
   const float4* bvh_nodes;       // 4 float4 per node, preorder with escape indices

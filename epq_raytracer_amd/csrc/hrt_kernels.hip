@@ -2126,7 +2126,7 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       if (q.split_k == 0) q.split_k = 1;
       const size_t lds = bvh_lds_bytes(p);
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
-      if (p.diag)
+      if (p.diag || p.probe)
         trace_bundle_bvh_lds<true><<<p.num_cus, 1024, lds, stream>>>(q);
       else
         trace_bundle_bvh_lds<false><<<p.num_cus, 1024, lds, stream>>>(q);
@@ -2146,7 +2146,7 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       const size_t lds = wq_lds_bytes(p, &q.wq_ncap, &q.wq_tcap);
       if (p.wq_ncap) q.wq_ncap = std::min(q.wq_ncap, std::max(128u, p.wq_ncap & ~63u));  // HRT_OPT_WQ_NODE_CAP
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
-      if (p.diag)
+      if (p.diag || p.probe)
         trace_bundle_wq<true><<<p.num_cus, 1024, lds, stream>>>(q);
       else
         trace_bundle_wq<false><<<p.num_cus, 1024, lds, stream>>>(q);
@@ -2163,12 +2163,12 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       q.coop = p.coop && q.split_k == 1 && p.pc.num_meshes <= 62 ? 1u : 0u;
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
       if (block == 512) {
-        if (p.diag)
+        if (p.diag || p.probe)
           trace_bundle_cull_lds<512, true><<<2 * p.num_cus, 512, lds, stream>>>(q);
         else
           trace_bundle_cull_lds<512, false><<<2 * p.num_cus, 512, lds, stream>>>(q);
       } else {
-        if (p.diag)
+        if (p.diag || p.probe)
           trace_bundle_cull_lds<1024, true><<<p.num_cus, 1024, lds, stream>>>(q);
         else
           trace_bundle_cull_lds<1024, false><<<p.num_cus, 1024, lds, stream>>>(q);

@@ -13,7 +13,7 @@ bash tools/pmc.sh $TAG/pmc 0 > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -2
 cp $OUT/pmc/pmc_traffic.json profiles/pmc_traffic.json
 timeout -k 10 600 python3 bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --cpu-seconds 0 "$@" > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --cpu-seconds 0 --steps 20 "$@" > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
 find $OUT/prof -name '*kernel_stats.csv' -exec cat {} \;
 timeout -k 10 300 python3 tools/tile_profile.py > $OUT/tile_profile.json 2>&1 || { echo "tile profile failed"; tail -20 $OUT/tile_profile.json; exit 1; }
 timeout -k 10 300 python3 tools/frames.py --frames 8 > $OUT/frames.json 2>&1 || { echo "frames failed"; tail -20 $OUT/frames.json; exit 1; }
