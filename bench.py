@@ -78,7 +78,7 @@ def main():
     from epq_raytracer_amd import _lib, rowtiles
 
     W, H = args.width, args.height
-    camera, settings = E.PRESETS[args.scene]()
+    camera, settings = E.preset(args.scene)
     settings.num_samples, settings.max_bounces = args.spp, args.bounces
     partition = (args.row_tile, rank, world) if dist_on else None
     ctx = E.HrtContext((W, H), device=device, mode=_lib.MODE_RGBA8, partition=partition)

@@ -375,6 +375,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   ctx->bvh_built_leaf = std::max(1u, std::min(ctx->bvh_leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
   ctx->bvh_rel_t = bvh.rel_t;
   ctx->bvh_info[5] = (uint32_t)(bvh.band_list.size() / 2);
+  ctx->bvh_info[6] = (uint32_t)std::min(1e9, bvh.sah_tri_frac * 1000.0 + 0.5);
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
   if (!keep_rays) ctx->n_rays = n_rays;
   ctx->plan_valid = false;  // tile costs describe the old scene
@@ -442,6 +443,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.bvh_irregular = ctx->bvh_irregular;
   p.bvh_band_off = ctx->bvh_band_off;
   p.bvh_dir_res = ctx->bvh_dir_res;
+  p.bvh_sah_milli = ctx->bvh_info[6];
   p.bvh_band = ctx->bvh_band;
   p.bvh_entries = ctx->bvh_entries;
   p.bvh_keybase = ctx->bvh_keybase;

@@ -442,6 +442,24 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
     Builder bld{entries, leaf_size, out};
     bld.build(0, (uint32_t)entries.size(), tris);
   }
+  // hierarchy quality: sum over leaves of area(leaf box) / area(root box) x leaf triangles = the
+  // expected leaf triangle tests of a uniform random line through the scene, per entry
+  if (out.n_nodes && out.n_prims) {
+    auto area = [&](uint32_t k) {
+      const float* r = &out.nodes[(size_t)k * 16];
+      const double ex = std::max(0.0, (double)r[4] - r[0]), ey = std::max(0.0, (double)r[5] - r[1]),
+                   ez = std::max(0.0, (double)r[6] - r[2]);
+      return 2.0 * (ex * ey + ey * ez + ex * ez);
+    };
+    const double root = area(0);
+    double tests = 0.0;
+    for (uint32_t k = 0; k < out.n_nodes; ++k) {
+      uint32_t info;
+      std::memcpy(&info, &out.nodes[(size_t)k * 16 + 14], 4);
+      if (info >> 27) tests += (info >> 27) * (root > 0.0 ? area(k) / root : 1.0);
+    }
+    out.sah_tri_frac = tests / out.n_prims;
+  }
   out.dir_res = (uint32_t)dir_res_for(out.n_prims);
   build_band_lists(out);
   // t-slack of the box test for a lane at distance <= R: abs = abs_coef R, rel

@@ -40,6 +40,7 @@ struct BvhHost {
   std::vector<uint32_t> key_base;   // per mesh: scan key of (m, i) = key_base[m] + i (mod 2^32)
   std::vector<uint32_t> band_off;   // 6 dir_res^2 + 1 offsets into band_list
   uint32_t dir_res = 64;            // direction cells per face edge (dir_res_for)
+  double sah_tri_frac = 0.0;        // expected leaf triangle tests of a uniform random ray / entries
   std::vector<uint32_t> band_list;  // 2 words per entry: prim | n^x << 18, n^y | n^z << 16 (kBand*)
   std::vector<float> wq_nodes;      // BUNDLE_WQ's 48 B node image (make_wq_nodes)
   bool wq_ok = false;               // the image exists (at most 65535 nodes)

@@ -54,6 +54,7 @@ struct TraceParams {
   const float4* bvh_irregular;   // 4 float4 per entry outside the analysis (tested for every ray)
   const uint32_t* bvh_band_off;  // 6 bvh_dir_res^2 + 1 offsets: grazing-band prims per direction cell
   uint32_t bvh_dir_res;          // direction cells per cube-map face edge
+  uint32_t bvh_sah_milli;        // hierarchy quality (HRT_SCENE_BVH_SAH_MILLI)
   const uint2* bvh_band;         // 8 B per entry (hrt_bvh.h kBand*): prim index, quantized n^
   const uint32_t* bvh_entries;   // per leaf prim: triangle index | mesh << 26 (BUNDLE_BVH_LDS)
   const uint32_t* bvh_keybase;   // per mesh: key = keybase[m] + triangle index

@@ -2042,11 +2042,15 @@ int resolve_variant(const TraceParams& p, int variant) {
     // profiles/r01g_*: island 21.4 (LDS) vs 23.7 ms, cave 112 vs 120 ms; BVH from ~4K triangles.
     // BUNDLE_WQ when its node stacks get >= 768 pairs (profiles/r01m_*: island, 1,024 pairs, 8.1 vs
     // 15.6 ms; cave, 576 pairs with the 48 B node image: 36-39 vs 31-34 ms, r01o)
+    // A poor hierarchy (large overlapping triangles, HRT_SCENE_BVH_SAH_MILLI > 100) is left to the
+    // wave-level culls: triangle soups of 256 / 1K / 4K / 16K run 2.5-5x faster culled
+    // (profiles/r01p_soup_sweep.log).
     uint32_t ncap = 0;
-    const bool wq = wq_lds_bytes(p, &ncap, nullptr) && ncap >= 768 && p.pc.num_meshes <= 64;
+    const bool good_bvh = p.bvh_nodes && p.bvh_sah_milli <= 100;
+    const bool wq = good_bvh && wq_lds_bytes(p, &ncap, nullptr) && ncap >= 768 && p.pc.num_meshes <= 64;
     variant = p.cam_list_capacity < kAutoCullTris                   ? HRT_KERNEL_BUNDLE
               : wq                                                 ? HRT_KERNEL_BUNDLE_WQ
-              : p.cam_list_capacity >= kAutoBvhTris && p.bvh_nodes ? HRT_KERNEL_BUNDLE_BVH
+              : p.cam_list_capacity >= kAutoBvhTris && good_bvh    ? HRT_KERNEL_BUNDLE_BVH
               : lds_block(p.n_tris) != 0                ? HRT_KERNEL_BUNDLE_CULL_LDS
                                                                  : HRT_KERNEL_BUNDLE_CULL;
   }

@@ -10,7 +10,7 @@ import numpy as np
 
 from .app import RayTracingApp
 from .pipeline import RayTracerSettings
-from .scene import (Camera, CustomMaterial, InvisLightMaterial, LambertianMaterial, LightMaterial, MetalMaterial,
+from .scene import (Camera, CustomMaterial, InvisLightMaterial, LambertianMaterial, LightMaterial, Mesh, MetalMaterial,
                     RayTracingMesh, Sphere, load_asset, subdivide)
 
 F = np.float32
@@ -121,11 +121,24 @@ def scaled_preset(name: str, k: int):
     return cam, settings
 
 
+def soup_scene(n: int, seed: int = 0x5EED):
+    """SURVEY.md 8(d)'s roofline-sweep scene: n triangles with vertices uniform in [-10, 10]^3 (seed
+    0x5EED), one Lambertian 0.5 mesh, environment light on, camera at (0, 0, -25) looking +z."""
+    rng = np.random.default_rng(seed)
+    v = rng.uniform(-10.0, 10.0, size=(n * 3, 3)).astype(np.float32)
+    mesh = Mesh(v, np.arange(n * 3, dtype=np.uint32))
+    cam = Camera([0.0, 0.0, -25.0], [0.0, 0.0, 1.0])
+    return cam, RayTracerSettings(num_samples=1, max_bounces=8, use_environment_lighting=True,
+                                  mesh_data=[RayTracingMesh(mesh, LambertianMaterial([0.5, 0.5, 0.5]))], up=cam.up)
+
+
 def preset(name: str):
-    """PRESETS[name]() or, for "<preset>@<k>", scaled_preset(preset, k)."""
+    """PRESETS[name]() or, for "<preset>@<k>", scaled_preset(preset, k); "soup<n>" = soup_scene(n)."""
     if "@" in name:
         base, k = name.split("@")
         return scaled_preset(base, int(k))
+    if name.startswith("soup") and name[4:].isdigit():
+        return soup_scene(int(name[4:]))
     return PRESETS[name]()
 
 

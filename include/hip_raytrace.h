@@ -152,9 +152,10 @@ typedef struct hrt_context hrt_context;
 /* Trace kernel variants (HRT_OPT_KERNEL_VARIANT).  All produce byte-identical frames and counters;
  * they differ only in how much of the reference's brute-force work they prove unnecessary. */
 typedef enum hrt_kernel {
-  HRT_KERNEL_AUTO = 0,        /* BUNDLE below 256 mesh triangles; then BUNDLE_WQ while the hierarchy fits
-                                 LDS; else BUNDLE_CULL_LDS while the triangle buffer fits LDS (else
-                                 BUNDLE_CULL) below 4096; BUNDLE_BVH above */
+  HRT_KERNEL_AUTO = 0,        /* BUNDLE below 256 mesh triangles; then, with a useful hierarchy
+                                 (HRT_SCENE_BVH_SAH_MILLI <= 100), BUNDLE_WQ while it fits LDS; else
+                                 BUNDLE_CULL_LDS while the triangle buffer fits LDS (else BUNDLE_CULL)
+                                 below 4096 triangles (any count for a poor hierarchy); BUNDLE_BVH above */
   HRT_KERNEL_LITERAL = 1,     /* raytracing.glsl's loop shape, the full test on every triangle */
   HRT_KERNEL_BRUTE = 2,       /* fused sample/bounce loop, two-stage exact pre-test, triangles via SGPRs */
   HRT_KERNEL_BRUTE_LDS = 3,   /* BRUTE with the scene resident in LDS (falls back to BRUTE above 160 KiB) */
@@ -243,7 +244,10 @@ typedef enum hrt_scene_info {
   HRT_SCENE_BVH_NEVER = 3,      /* entries with a zero normal, which the reference never accepts */
   HRT_SCENE_BVH_BUILT = 4,      /* 1 if built (0: > 64 meshes or > 2^18 entries -> BUNDLE_BVH runs BUNDLE_CULL) */
   HRT_SCENE_BVH_BAND_ENTRIES = 5, /* grazing-band list entries over all direction cells */
-  HRT_NUM_SCENE_INFO = 6
+  HRT_SCENE_BVH_SAH_MILLI = 6,  /* 1000 x the expected leaf triangle tests of a uniform random ray per
+                                   entry (surface-area estimate): < ~30 for a useful hierarchy; large
+                                   overlapping triangles (a soup) give ~500, and auto then culls instead */
+  HRT_NUM_SCENE_INFO = 7
 } hrt_scene_info;
 
 uint32_t hrt_abi_version(void);

@@ -462,6 +462,25 @@ def test_large_scene_auto_picks_bvh():
         assert (gseg, gtt) == (seg, tt)
 
 
+@pytest.mark.parametrize("scene,expect", [("soup1024", _lib.KERNEL_BUNDLE_CULL_LDS), ("soup4096", _lib.KERNEL_BUNDLE_CULL),
+                                          ("island", _lib.KERNEL_BUNDLE_WQ), ("island@2", _lib.KERNEL_BUNDLE_BVH)])
+def test_auto_follows_hierarchy_quality(scene, expect):
+    """AUTO reads the hierarchy's surface-area estimate (HRT_SCENE_BVH_SAH_MILLI): triangle soups (large
+    overlapping triangles, ~500) are culled; island-like meshes (< 30) traverse the hierarchy."""
+    case = SceneCase(scene, (48, 40), 2, 8)
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context(variant=_lib.KERNEL_AUTO)
+    info = ctx.scene_info()
+    assert (info["bvh_sah_milli"] > 100) == scene.startswith("soup"), info
+    ctx.trace(case.push())
+    st = ctx.stats()
+    img = ctx.read(_lib.IMG_TRACE)
+    ctx.close()
+    assert st.last_kernel == expect, (st.last_kernel, expect)
+    assert np.array_equal(img, ref), mismatch_report(img, ref)
+    assert (st.segments, st.tri_tests) == (seg, tt)
+
+
 @pytest.mark.parametrize("leaf", [1, 2, 8, 16])
 def test_bvh_leaf_sizes(leaf):
     case = SceneCase("cave", (80, 48), 2, 8)
