@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """Benchmark: Mrays/s of the MI355X path tracer on the headline workload of BASELINE.json
-(island.obj, 1920x1080, 64 spp, 8 bounces) -- one "step" = one progressive frame: one trace dispatch
-(64 samples per pixel, rng_offset = frame index) + one accumulate dispatch (+ the row-tile gather of
-the framebuffer when N > 1).
+(island.obj, 1920x1080, 64 spp, 8 bounces) -- one "step" = one progressive frame: one trace of 64
+samples per pixel (rng_offset = frame index) + one accumulate.  The K timed steps are the frame loop
+of compute_n_then_render (src/raytracing_app.rs:198-227): one hrt_compute_n call of K frames (the
+persistent kernel traces up to --frames-per-launch of them per launch, each frame its own image, the
+combiner folding them in order -- byte for byte the per-frame loop), then, when N > 1, the row-tile
+gather of the accumulated framebuffer for its present.  --frames-per-launch 1 runs the realtime loop
+instead (compute_then_render: trace + accumulate + gather per frame).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -33,7 +37,7 @@ BYTES_PER_PIXEL_FRAME = 32  # 16 B ray centre + 4 B trace store + 12 B combiner 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene", default="island")
     ap.add_argument("--width", type=int, default=1920)
@@ -43,6 +47,9 @@ def parse():
     ap.add_argument("--variant", type=int, default=0,
                     help="hrt_kernel: 0 auto, 1 literal, 2 brute, 3 brute_lds, 4 bundle, 5 bundle_cull")
     ap.add_argument("--row-tile", type=int, default=16)
+    ap.add_argument("--frames-per-launch", type=int, default=16,
+                    help="> 1: steps run as hrt_compute_n (compute_n_then_render) with up to this many frames per "
+                         "trace launch; 1: one trace + accumulate (+ gather) dispatch per step (compute_then_render)")
     ap.add_argument("--verify", action="store_true",
                     help="N>1: rank 0 re-renders all frames on one full-frame context and compares the gathered frame")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -85,6 +92,8 @@ def main():
     raytrace = E.RayTracePipeline(ctx, (W, H), settings)
     diffuse = E.DiffusePipeline(ctx, (W, H))
     ctx.set_option(_lib.OPT_KERNEL_VARIANT, args.variant)
+    fpl = max(1, args.frames_per_launch)
+    ctx.set_option(_lib.OPT_FRAMES_PER_LAUNCH, fpl)
     raytrace.init()
     diffuse.next_frame(0, raytrace.image())
     frame = 1
@@ -92,17 +101,28 @@ def main():
     local = torch.empty((ctx.local_rows, W, 4), dtype=torch.uint8, device=coll_dev) if dist_on else None
     full = None
 
-    def step():
-        nonlocal frame, full
-        raytrace.compute(camera, frame)
-        diffuse.next_frame(frame, raytrace.image())
-        frame += 1
+    def present():
+        nonlocal full
         if dist_on:  # the framebuffer gather: one all-gather of equal-size row-tile blocks
             ctx.read_into(_lib.IMG_ACCUM, _lib.FMT_RGBA8, local.data_ptr(), local.numel())
             full = rowtiles.gather_frame(local, H, args.row_tile)
 
-    for _ in range(args.warmup):
-        step()
+    def steps(k):
+        nonlocal frame
+        if k <= 0:
+            return
+        if fpl > 1:  # compute_n_then_render(k): k frames, then one present
+            ctx.compute_n(raytrace.push_constants(camera, frame, False), k)
+            frame += k
+            present()
+            return
+        for _ in range(k):  # compute_then_render per frame
+            raytrace.compute(camera, frame)
+            diffuse.next_frame(frame, raytrace.image())
+            frame += 1
+            present()
+
+    steps(args.warmup)
     ctx.synchronize()
     torch.cuda.synchronize()
     ctx.reset_stats()
@@ -111,8 +131,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    steps(args.steps)
     ctx.synchronize()
     torch.cuda.synchronize()
     if dist_on:
@@ -121,7 +140,10 @@ def main():
 
     st = ctx.stats()
     segs, tests = st.segments, st.tri_tests
-    kern_ms = st.total_trace_ms / max(st.traces, 1)
+    kern_ms = st.total_trace_ms / max(st.traces, 1)  # per frame (a launch of f frames counts f traces)
+    launches = -(-args.steps // fpl) if fpl > 1 else args.steps
+    last_frame = frame - 1
+    last_trace = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8) if rank == 0 and world == 1 else None
     kernel_sym = _lib.kernel_symbol(st.last_kernel, st.last_block)  # what HRT_KERNEL_AUTO resolved to
     if dist_on:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=coll_dev)
@@ -137,10 +159,10 @@ def main():
         ms_per_step = elapsed * 1e3 / args.steps
         value = segs_all / elapsed / 1e6
         # roofline of the dominant kernel (trace), rank 0's launches: algorithmic FLOP / launch time
-        tests_per_launch = tests / max(st.traces, 1)
+        tests_per_frame = tests / max(st.traces, 1)
         # reference-equivalent work: 38 FLOP per triangle test the reference performs;
         # the tuned kernel skips most of them exactly, so this rate can exceed the hardware peak.
-        algorithmic_tf = FLOP_PER_TEST * tests_per_launch / (kern_ms * 1e-3) / 1e12
+        algorithmic_tf = FLOP_PER_TEST * tests_per_frame / (kern_ms * 1e-3) / 1e12
         pix_local = ctx.local_rows * W
         algo_bytes = BYTES_PER_PIXEL_FRAME * pix_local + (len(raytrace.tris) * 64 + len(raytrace.meshes) * 80)
         traffic = None
@@ -161,7 +183,7 @@ def main():
                 basis = "executed (rocprofv3 PMC FLOP count per launch / live launch time)"
             elif same_kernel and per_test:
                 # this rank's launch: the profiled kernel's FLOPs per reference triangle test x its own tests
-                executed_flops = per_test * tests_per_launch
+                executed_flops = per_test * tests_per_frame
                 if exact and pmc.get("hbm_bytes_per_trace_launch"):
                     traffic = pmc["hbm_bytes_per_trace_launch"] * ctx.local_rows / H
                 basis = ("executed (rocprofv3 PMC FLOPs per reference test of this kernel on " +
@@ -187,7 +209,11 @@ def main():
             "data": "synthetic: reference scene preset (island.obj geometry + src/main.rs materials/camera), "
                     "deterministic RNG seeds rng_offset = frame index",
             "config": {"workload": f"{args.scene}.obj {W}x{H} {args.spp}spp {args.bounces}-bounce, 1 frame/step "
-                                   f"(trace + accumulate{' + row-tile gather' if dist_on else ''})",
+                                   + (f"(trace + accumulate; the {args.steps} steps as compute_n_then_render: "
+                                      f"{launches} trace launch(es) of <= {fpl} frames"
+                                      f"{', then the row-tile gather' if dist_on else ''})" if fpl > 1 else
+                                      f"(trace + accumulate{' + row-tile gather' if dist_on else ''} per frame)"),
+                       "frames_per_launch": fpl if fpl > 1 else 1,
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                        "parallelism": (f"row-tiles{world}x{args.row_tile} ({args.dist_backend} gather)"
                                        if dist_on else "single-gpu"),
@@ -202,14 +228,19 @@ def main():
                          "traffic": traffic, "achieved_basis": basis,
                          "algorithmic_tflops": round(algorithmic_tf, 3),
                          "kernel": kernel_sym,
-                         "kernel_ms": round(kern_ms, 3), "flop_per_test": FLOP_PER_TEST,
-                         "tests_per_launch": int(tests_per_launch), "pmc_source": pmc_note},
+                         "kernel_ms": round(kern_ms, 3),
+                         "launch_ms": round(kern_ms * args.steps / launches, 3),
+                         "kernel_ms_basis": "per frame: launch time / frames per launch (HIP events on the "
+                                            "context's stream)",
+                         "flop_per_test": FLOP_PER_TEST,
+                         "tests_per_frame": int(tests_per_frame), "pmc_source": pmc_note},
             "hbm_roofline": {"achieved": round(algo_bytes / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(algo_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
-                             "algorithmic_bytes_per_launch": algo_bytes, "traffic": traffic},
+                             "algorithmic_bytes_per_frame": algo_bytes, "traffic": traffic},
         }
         if world == 1 and args.cpu_seconds > 0:
-            line["cpu_baseline"], line["parity_sample"] = cpu_baseline(args, ctx, raytrace, camera)
+            line["cpu_baseline"], line["parity_sample"] = cpu_baseline(args, raytrace, camera, last_frame,
+                                                                       last_trace)
         if dist_on and args.verify:
             line["gather_check"] = verify_gather(args, full, settings, camera, device, frame - 1)
         print(json.dumps(line), flush=True)
@@ -241,16 +272,16 @@ def verify_gather(args, full, settings, camera, device, last_frame):
             "pixels_differing": int(np.any(got != ref, axis=-1).sum())}
 
 
-def cpu_baseline(args, ctx, raytrace, camera):
+def cpu_baseline(args, raytrace, camera, last_frame, gpu):
     """The oracle (oracle/rt_oracle.c, OpenMP) on a bounded sample of the same workload: whole rows
-    spread evenly over the frame, frame rng_offset = 1.  Also checks those rows of the GPU frame
-    byte for byte against it (the same rows, traced again on the GPU with rng_offset = 1)."""
+    spread evenly over the last timed frame (rng_offset = last_frame).  Also checks those rows of the
+    GPU's trace image of that frame (as the timed loop left it) byte for byte against it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from epq_raytracer_amd import _lib
 
     W, H = args.width, args.height
-    pc = raytrace.push_constants(camera, 1, False)
+    pc = raytrace.push_constants(camera, last_frame, False)
     rays = raytrace.rays
     threads = pyoracle.num_threads()
     # calibrate on one row, then pick a row count for ~cpu_seconds
@@ -267,14 +298,12 @@ def cpu_baseline(args, ctx, raytrace, camera):
         cpu_img[y] = img[y]
         segs += s
     dt = time.perf_counter() - t
-    # GPU frame with the same rng_offset, same rows
-    ctx.trace(pc)
-    gpu = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
     same = bool(np.array_equal(gpu[rows], cpu_img[rows]))
     base = {"value": round(segs / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{len(rows)} of {H} rows (evenly spaced) of the same frame (rng_offset=1), {segs} segments, "
+            "sample": f"{len(rows)} of {H} rows (evenly spaced) of the same frame (rng_offset={last_frame}), "
+                      f"{segs} segments, "
                       f"{dt:.1f} s on {threads} OpenMP threads (oracle/rt_oracle.c -O2 -ffp-contract=off)"}
-    parity = {"rows_checked": int(len(rows)), "bit_exact": same}
+    parity = {"rows_checked": int(len(rows)), "frame": last_frame, "bit_exact": same}
     return base, parity
 
 

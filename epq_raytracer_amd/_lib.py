@@ -73,6 +73,7 @@ IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
 OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP, OPT_WQ_NODE_CAP, OPT_PROBE = 5, 6, 7, 8, 9, 10, 11
+OPT_FRAMES_PER_LAUNCH = 12
 # hrt_kernel (include/hip_raytrace.h)
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
 KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS, KERNEL_BUNDLE_BVH_LDS, KERNEL_BUNDLE_WQ = 6, 7, 8, 9
@@ -99,7 +100,7 @@ SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh
 
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).
 EXPORTED_SYMBOLS = (
-    "hrt_abi_version", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate",
+    "hrt_abi_version", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate", "hrt_compute_n",
     "hrt_read_image", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
     "hrt_get_diagnostics", "hrt_get_tile_profile", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
     "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory",
@@ -139,6 +140,7 @@ def load() -> ctypes.CDLL:
         "hrt_set_scene": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32]),
         "hrt_trace": (c_int32, [P, POINTER(PushConstants)]),
         "hrt_accumulate": (c_int32, [P, c_uint32]),
+        "hrt_compute_n": (c_int32, [P, POINTER(PushConstants), c_uint32]),
         "hrt_read_image": (c_int32, [P, c_uint32, c_uint32, P, c_size_t]),
         "hrt_get_layout": (c_int32, [P, POINTER(Layout)]),
         "hrt_synchronize": (c_int32, [P]),

@@ -58,11 +58,15 @@ def compute_then_render(app: RayTracingApp, frame_time: float = 0.0) -> None:
 
 
 def compute_n_then_render(app: RayTracingApp, num_renders: int) -> None:
-    """src/raytracing_app.rs:196-227 (N frames chained without a host wait, then one present)."""
+    """src/raytracing_app.rs:196-227 (N frames chained without a host wait, then one present).
+
+    The frame loop is one hrt_compute_n call: the same traces and accumulates byte for byte, with the
+    persistent kernels tracing several frames per launch."""
     raytrace, diffuse, render = app.pipeline
-    for _ in range(num_renders):
-        raytrace.compute(app.camera, app.frame)
-        diffuse.next_frame(app.frame, raytrace.image())
-        app.frame += 1
+    if num_renders > 0:
+        if diffuse.ctx is not raytrace.ctx:
+            raise ValueError("the trace and the accumulator must share one context")
+        raytrace.ctx.compute_n(raytrace.push_constants(app.camera, app.frame, False), num_renders)
+        app.frame += num_renders
     if render is not None:
         render(diffuse.image())

@@ -35,6 +35,7 @@ constexpr int kNumCounters = 3 + HRT_NUM_DIAG;  // segments, triangle tests, wav
 
 struct EventPair {
   hipEvent_t start = nullptr, stop = nullptr;
+  uint32_t frames = 1;  // frames the timed launch traced
 };
 
 }  // namespace
@@ -69,6 +70,9 @@ struct hrt_context {
   uint32_t coop = 1;      // HRT_OPT_COOP
   uint32_t wq_node_cap = 0;  // HRT_OPT_WQ_NODE_CAP (0 = auto)
   uint32_t probe = 1;        // HRT_OPT_PROBE
+  uint32_t frames_per_launch = 16;  // HRT_OPT_FRAMES_PER_LAUNCH (hrt_compute_n)
+  void* frame_stack = nullptr;      // hrt_compute_n: frame_stack_frames trace images
+  uint32_t frame_stack_frames = 0;
   uint32_t num_cus = 0;
   uint32_t* cam_meta = nullptr;   // bundle variants: cam_start[n_meshes], cam_count[n_meshes]
   uint32_t cam_capacity = 0;      // sum of mesh lengths
@@ -148,7 +152,7 @@ hrt_status harvest_events(hrt_context* ctx) {
     HRT_HIP(ctx, hipEventSynchronize(ev.stop));
     float ms = 0.0f;
     HRT_HIP(ctx, hipEventElapsedTime(&ms, ev.start, ev.stop));
-    ctx->last_ms = ms;
+    ctx->last_ms = ms / (float)ev.frames;  // per frame
     ctx->total_ms += ms;
     ctx->event_pool.push_back(ev);
   }
@@ -276,6 +280,7 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
   free_dev(ctx->sched);
   free_dev(ctx->tile_cost);
   free_dev(ctx->item_buf);
+  free_dev(ctx->frame_stack);
   for (auto& im : ctx->imports) (void)hipDestroyExternalMemory(im.mem);
   for (auto& ev : ctx->event_pool) {
     (void)hipEventDestroy(ev.start);
@@ -386,21 +391,21 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   return HRT_OK;
 }
 
-extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) {
-  if (!ctx || !pc) return HRT_ERR_INVALID_ARGUMENT;
-  hrt_status st = bind(ctx);
-  if (st != HRT_OK) return st;
-  if (pc->init) {  // RayTracePipeline::init, src/raytrace_pipeline.rs:190-213
-    HRT_HIP(ctx, hrt::launch_clear(ctx->trace8, ctx->trace32, ctx->npix(), ctx->stream));
-    return HRT_OK;
-  }
-  if (!ctx->scene_set) return fail(ctx, HRT_ERR_NO_SCENE, "hrt_trace: hrt_set_scene has not been called");
+namespace {
+
+// Validates a dispatch's push block against the context (hrt_trace / hrt_compute_n).
+hrt_status check_dispatch(hrt_context* ctx, const hrt_push_constants* pc, const char* who) {
+  if (!ctx->scene_set) return fail(ctx, HRT_ERR_NO_SCENE, std::string(who) + ": hrt_set_scene has not been called");
   if (pc->width != ctx->width || pc->height != ctx->height)
-    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_trace: push constant width/height differ from the context");
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, std::string(who) + ": push constant width/height differ from the context");
   if (pc->num_spheres < 0 || (uint32_t)pc->num_spheres > ctx->n_spheres || pc->num_meshes < 0 ||
       (uint32_t)pc->num_meshes > ctx->n_meshes)
-    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_trace: num_spheres/num_meshes exceed the uploaded scene");
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, std::string(who) + ": num_spheres/num_meshes exceed the uploaded scene");
+  return HRT_OK;
+}
 
+// The kernel argument block of a dispatch of pc into the context's trace image.
+hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc) {
   hrt::TraceParams p{};
   p.rays = ctx->rays;
   p.spheres = ctx->spheres;
@@ -410,11 +415,7 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.img32 = ctx->trace32;
   p.counters = ctx->counters_on ? ctx->counters : nullptr;
   p.diag = ctx->diag_on ? ctx->counters + 3 : nullptr;
-  if (ctx->diag_on && !ctx->tile_cycles)
-    HRT_HIP(ctx, hipMalloc((void**)&ctx->tile_cycles, ctx->num_tiles() * 4 * sizeof(unsigned long long)));
   p.tile_cycles = ctx->diag_on ? ctx->tile_cycles : nullptr;
-  if (ctx->diag_on)
-    HRT_HIP(ctx, hipMemsetAsync(ctx->tile_cycles, 0, ctx->num_tiles() * 4 * sizeof(unsigned long long), ctx->stream));
   p.pc = *pc;
   p.local_rows = ctx->local_rows;
   p.row_tile = ctx->row_tile;
@@ -454,8 +455,24 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   p.bvh_rel_t = ctx->bvh_rel_t;
   p.bvh_n_irregular = ctx->bvh_info[2];
   p.bvh_max_leaf = ctx->bvh_built_leaf;
-  const int variant = ctx->variant;
+  p.n_frames = 1;
+  p.frame_stride = ctx->npix();
+  return p;
+}
 
+bool persistent_kernel(int k) {
+  return k == HRT_KERNEL_BUNDLE_WQ || k == HRT_KERNEL_BUNDLE_CULL_LDS || k == HRT_KERNEL_BUNDLE_BVH_LDS;
+}
+
+// One trace launch of p.n_frames frames (timed by a HIP event pair counted as that many traces).
+hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p) {
+  if (ctx->diag_on && !ctx->tile_cycles) {
+    HRT_HIP(ctx, hipMalloc((void**)&ctx->tile_cycles, ctx->num_tiles() * 4 * sizeof(unsigned long long)));
+    p.tile_cycles = ctx->tile_cycles;
+  }
+  if (ctx->diag_on)
+    HRT_HIP(ctx, hipMemsetAsync(ctx->tile_cycles, 0, ctx->num_tiles() * 4 * sizeof(unsigned long long), ctx->stream));
+  const int variant = ctx->variant;
   EventPair ev;
   if (!ctx->event_pool.empty()) {
     ev = ctx->event_pool.back();
@@ -464,14 +481,14 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
     HRT_HIP(ctx, hipEventCreate(&ev.start));
     HRT_HIP(ctx, hipEventCreate(&ev.stop));
   }
+  ev.frames = p.n_frames > 1 ? p.n_frames : 1u;
   // First trace of a persistent kernel (no tile costs yet): a 1-sample probe trace into the scratch
   // image measures the tiles' relative costs so that this trace already follows a plan (HRT_OPT_PROBE).
   const int resolved = hrt::resolve_variant(p, variant);
-  if (ctx->probe && !ctx->plan_valid && ctx->num_tiles() >= 1024 &&
-      (resolved == HRT_KERNEL_BUNDLE_WQ || resolved == HRT_KERNEL_BUNDLE_CULL_LDS ||
-       resolved == HRT_KERNEL_BUNDLE_BVH_LDS)) {
+  if (ctx->probe && !ctx->plan_valid && ctx->num_tiles() >= 1024 && persistent_kernel(resolved)) {
     hrt::TraceParams q = p;
     q.pc.num_samples = 1;
+    q.n_frames = 1;
     q.img8 = ctx->trace8 ? reinterpret_cast<uint32_t*>(ctx->scratch) : nullptr;
     q.img32 = ctx->trace32 ? reinterpret_cast<float4*>(ctx->scratch) : nullptr;
     q.counters = nullptr;
@@ -479,24 +496,85 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
     q.tile_cycles = nullptr;
     q.probe = 1u;
     int ran = 0, blk = 0;
-    if (hipError_t pe = hrt::launch_trace(q, variant, ctx->stream, &ran, &blk); pe != hipSuccess)
+    if (hipError_t pe = hrt::launch_trace(q, variant, ctx->stream, &ran, &blk); pe != hipSuccess) {
+      ctx->event_pool.push_back(ev);
       return hip_fail(ctx, pe, "probe trace launch");
+    }
     p.plan_valid = 1u;
   }
   HRT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
   hipError_t e = hrt::launch_trace(p, variant, ctx->stream, &ctx->last_kernel, &ctx->last_block);
   // the persistent kernels recorded this trace's tile costs: the next one can follow a plan
-  ctx->plan_valid = e == hipSuccess && (ctx->last_kernel == HRT_KERNEL_BUNDLE_CULL_LDS ||
-                                        ctx->last_kernel == HRT_KERNEL_BUNDLE_BVH_LDS ||
-                                        ctx->last_kernel == HRT_KERNEL_BUNDLE_WQ);
+  ctx->plan_valid = e == hipSuccess && persistent_kernel(ctx->last_kernel);
   if (e != hipSuccess) {
     ctx->event_pool.push_back(ev);
     return hip_fail(ctx, e, "trace kernel launch");
   }
   HRT_HIP(ctx, hipEventRecord(ev.stop, ctx->stream));
   ctx->pending.push_back(ev);
-  ctx->traces++;
+  ctx->traces += ev.frames;
   if (ctx->pending.size() > 256) return harvest_events(ctx);  // bound the pending list
+  return HRT_OK;
+}
+
+}  // namespace
+
+extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) {
+  if (!ctx || !pc) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  if (pc->init) {  // RayTracePipeline::init, src/raytrace_pipeline.rs:190-213
+    HRT_HIP(ctx, hrt::launch_clear(ctx->trace8, ctx->trace32, ctx->npix(), ctx->stream));
+    return HRT_OK;
+  }
+  if ((st = check_dispatch(ctx, pc, "hrt_trace")) != HRT_OK) return st;
+  hrt::TraceParams p = make_params(ctx, pc);
+  return launch_frames(ctx, p);
+}
+
+extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* pc, uint32_t n) {
+  if (!ctx || !pc) return HRT_ERR_INVALID_ARGUMENT;
+  if (pc->init) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_compute_n: init dispatches go through hrt_trace");
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  if ((st = check_dispatch(ctx, pc, "hrt_compute_n")) != HRT_OK) return st;
+  hrt::TraceParams p = make_params(ctx, pc);
+  const size_t np = ctx->npix(), px_bytes = ctx->trace8 ? 4 : 16;
+  // Frames per launch: up to HRT_OPT_FRAMES_PER_LAUNCH, and at most 1 GiB of frame images.
+  const uint32_t cap = (uint32_t)std::max<size_t>(
+      1, std::min<size_t>(ctx->frames_per_launch, ((size_t)1 << 30) / std::max<size_t>(np * px_bytes, 1)));
+  const bool batch = persistent_kernel(hrt::resolve_variant(p, ctx->variant)) && cap > 1 && n > 1;
+  if (batch && ctx->frame_stack_frames < std::min(cap, n)) {
+    free_dev(ctx->frame_stack);
+    ctx->frame_stack_frames = 0;
+    HRT_HIP(ctx, hipMalloc(&ctx->frame_stack, (size_t)std::min(cap, n) * np * px_bytes));
+    ctx->frame_stack_frames = std::min(cap, n);
+  }
+  for (uint32_t done = 0; done < n;) {
+    // near-equal launches: ceil(remaining / cap) of them
+    const uint32_t left = n - done, launches = batch ? (left + cap - 1) / cap : left;
+    const uint32_t nf = (left + launches - 1) / launches;
+    hrt::TraceParams q = p;
+    q.pc.rng_offset = pc->rng_offset + done;  // u32, wrapping like the per-frame loop's pushes
+    q.n_frames = nf;
+    q.plan_valid = ctx->plan_valid ? 1u : 0u;
+    if (nf > 1) {
+      q.img8 = ctx->trace8 ? reinterpret_cast<uint32_t*>(ctx->frame_stack) : nullptr;
+      q.img32 = ctx->trace32 ? reinterpret_cast<float4*>(ctx->frame_stack) : nullptr;
+    }
+    if ((st = launch_frames(ctx, q)) != HRT_OK) return st;
+    for (uint32_t f = 0; f < nf; ++f) {  // DiffusePipeline::next_frame(frame) in frame order
+      const uint32_t* t8 = nf > 1 && q.img8 ? q.img8 + f * np : ctx->trace8;
+      const float4* t32 = nf > 1 && q.img32 ? q.img32 + f * np : ctx->trace32;
+      HRT_HIP(ctx, hrt::launch_accumulate(ctx->accum8, t8, ctx->accum32, t32, np, q.pc.rng_offset + f, ctx->stream));
+      ctx->accumulates++;
+    }
+    if (nf > 1)  // the trace image holds the last frame, as after the per-frame loop
+      HRT_HIP(ctx, hipMemcpyAsync(ctx->trace8 ? (void*)ctx->trace8 : (void*)ctx->trace32,
+                                  static_cast<const char*>(ctx->frame_stack) + (size_t)(nf - 1) * np * px_bytes,
+                                  np * px_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    done += nf;
+  }
   return HRT_OK;
 }
 
@@ -762,6 +840,11 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
     case HRT_OPT_PROBE:
       if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "probe must be 0 or 1");
       ctx->probe = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_FRAMES_PER_LAUNCH:
+      if (value < 1 || value > 1024)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "frames per launch must be in [1, 1024]");
+      ctx->frames_per_launch = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_WQ_NODE_CAP:
       if (value != 0 && (value < 128 || value > (1 << 20)))

@@ -62,6 +62,10 @@ struct TraceParams {
   float bvh_abs_coef, bvh_rel_t;  // box-test t-slack (hrt_bvh.h)
   uint32_t bvh_max_leaf;         // largest leaf triangle count of the hierarchy
   uint32_t wq_ncap, wq_tcap;     // BUNDLE_WQ: per-wave node / triangle pair stack capacities (launch_trace)
+  // Frames per launch (persistent variants, hrt_compute_n): frame f (0 <= f < n_frames) uses
+  // rng_offset + f and writes img8 / img32 + f * frame_stride pixels.  0 or 1: one frame.
+  uint32_t n_frames;
+  size_t frame_stride;
 };
 
 // Launches the trace kernel(s); *ran / *block receive the resolved hrt_kernel and workgroup size.

@@ -213,8 +213,9 @@ __device__ __forceinline__ bool shade_step(const Scene& sc, const hrt_push_const
   return true;
 }
 
-__device__ __forceinline__ void store_pixel(const TraceParams& P, uint32_t x, uint32_t lr, f3 col) {
-  const size_t idx = (size_t)lr * P.pc.width + x;
+__device__ __forceinline__ void store_pixel(const TraceParams& P, uint32_t x, uint32_t lr, f3 col,
+                                            uint32_t frame = 0) {
+  const size_t idx = (size_t)lr * P.pc.width + x + frame * P.frame_stride;
   if (P.img8) {
     P.img8[idx] = unorm8(col.x) | (unorm8(col.y) << 8) | (unorm8(col.z) << 16) | (255u << 24);
   }
@@ -1457,7 +1458,8 @@ enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2, kBounceWq =
 
 template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, const CullSrc& csrc,
-                                                  const BvhSrc& bsrc, uint32_t* list_lds, Coop& co) {
+                                                  const BvhSrc& bsrc, uint32_t* list_lds, Coop& co,
+                                                  uint32_t frame = 0) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
   const hrt_push_constants& pc = P.pc;
   const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
@@ -1467,7 +1469,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   const uint32_t id = active ? x + y * pc.width : 0u;
   const uint64_t tile_t0 = (D && P.tile_cycles) ? __builtin_readcyclecounter() : 0;
   f3 colour = mk(0.0f, 0.0f, 0.0f);
-  uint32_t state = pc.rng_offset * 719393u + id;
+  uint32_t state = (pc.rng_offset + frame) * 719393u + id;  // raytracing.glsl:376, frame f of the launch
   f3 centre = mk(0.0f, 0.0f, 0.0f);
   if (active) {
     const float4 rc = sc.rays[id];
@@ -1551,7 +1553,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   if (co.w != 0) return;  // cooperative tile: wave 0 of the group writes the results
   if (active) {
     colour = colour / (float)pc.num_samples;
-    store_pixel(P, x, lr, colour);
+    store_pixel(P, x, lr, colour, frame);
   }
   flush_counters(P, segs, tests);
   if (D && P.tile_cycles && (threadIdx.x & 63) == 0) {  // lane 0 sits at the tile's (0, 0)
@@ -1664,13 +1666,16 @@ template <int BLOCK, bool CoopOk, class Body>
 __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long long* ex, uint32_t* s_item, Body&& body) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t tiles_x = (P.pc.width + 7) / 8, tiles = tiles_x * ((P.local_rows + 7) / 8);
-  const uint32_t n = P.items ? P.sched[1] : tiles;
+  // A launch of nf frames runs every item once per frame: work index t is item t / nf of frame t % nf,
+  // so each item's frames follow each other and the plan's longest-first order holds across frames.
+  const uint32_t nf = P.n_frames > 1 ? P.n_frames : 1u;
+  const uint32_t n = (P.items ? P.sched[1] : tiles) * nf;
   uint32_t first = 0;
   // Phase 1 (a plan with cooperative heavy tiles): the workgroup takes the heavy items [0, H) one
   // at a time, all its waves on the same tile (Coop).  The item index goes through LDS; at the loop
   // head each wave's lane 0 publishes its share of the previous tile's work units.
   if (CoopOk && P.items && P.coop) {
-    const uint32_t H = P.sched[2];
+    const uint32_t H = P.sched[2] * nf;
     first = H;
     Coop co{threadIdx.x >> 6, (uint32_t)BLOCK / 64, ex, 0u, 0u};
     uint32_t prev_tile = 0xFFFFFFFFu, prev_cost = 0;
@@ -1686,10 +1691,11 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
       const uint32_t h = __builtin_amdgcn_readfirstlane(*s_item);
       __syncthreads();
       if (h >= H) break;
-      const uint32_t tile = __builtin_amdgcn_readfirstlane(P.items[h]) & kItemTileMask;
+      const uint32_t hi = h / nf, hf = h - hi * nf;
+      const uint32_t tile = __builtin_amdgcn_readfirstlane(P.items[hi]) & kItemTileMask;
       const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
       co.work = 0;
-      body(tx * 8 + (lane & 7), ty * 8 + (lane >> 3), co);
+      body(tx * 8 + (lane & 7), ty * 8 + (lane >> 3), co, hf);
       prev_cost = __builtin_amdgcn_readfirstlane(co.work);
       prev_tile = tile;
     }
@@ -1718,8 +1724,9 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     }
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= n) break;
-    const uint32_t item = P.items ? __builtin_amdgcn_readfirstlane(P.items[t]) : 0u;
-    const uint32_t tile = P.items ? item & kItemTileMask : t, lk = (item >> 22) & 7u, sub = (item >> 25) & 63u;
+    const uint32_t ti = t / nf, tf = t - ti * nf;
+    const uint32_t item = P.items ? __builtin_amdgcn_readfirstlane(P.items[ti]) : 0u;
+    const uint32_t tile = P.items ? item & kItemTileMask : ti, lk = (item >> 22) & 7u, sub = (item >> 25) & 63u;
     const bool hot = item >> 31;  // heavy last time: issue priority over the light tiles' waves
     const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
     const uint32_t j = (sub << (6u - lk)) + lane;  // the tile pixel (row-major) of this lane
@@ -1728,7 +1735,7 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     const uint64_t t0 = __builtin_readcyclecounter();
     if (hot) __builtin_amdgcn_s_setprio(3);
     solo.work = 0;
-    body(x, lr, solo);
+    body(x, lr, solo, tf);
     if (hot) __builtin_amdgcn_s_setprio(0);
     // cost: the work count where the body keeps one (BUNDLE_CULL_LDS), else shader clocks / 16
     const uint64_t c = CoopOk ? (uint64_t)solo.work : (__builtin_readcyclecounter() - t0) >> 4;
@@ -1829,8 +1836,8 @@ __global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
   unsigned long long* ex = reinterpret_cast<unsigned long long*>(lds_tris + 3 * P.n_tris);
   for (uint32_t k = threadIdx.x; k < 3 * 64; k += BLOCK) ex[k] = ~0ull;
   __syncthreads();
-  tile_loop<BLOCK, true>(P, ex, &s_item, [&](uint32_t x, uint32_t lr, Coop& co) {
-    trace_fused_split<kBounceCull, D>(P, x, lr, CullLds{lds_tris}, BvhGlobal{}, nullptr, co);
+  tile_loop<BLOCK, true>(P, ex, &s_item, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f) {
+    trace_fused_split<kBounceCull, D>(P, x, lr, CullLds{lds_tris}, BvhGlobal{}, nullptr, co, f);
   });
 }
 
@@ -1846,8 +1853,8 @@ __global__ __launch_bounds__(1024) void trace_bundle_wq(TraceParams P) {
                  reinterpret_cast<uint32_t*>(base + 512) + P.wq_ncap, P.wq_ncap};
   __syncthreads();
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co) {
-    trace_fused_split<kBounceWq, D>(P, x, lr, CullGlobal{T, to_const(T)}, wq, nullptr, co);
+  tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f) {
+    trace_fused_split<kBounceWq, D>(P, x, lr, CullGlobal{T, to_const(T)}, wq, nullptr, co, f);
   });
 }
 
@@ -1865,9 +1872,9 @@ __global__ __launch_bounds__(1024) void trace_bundle_bvh_lds(TraceParams P) {
   for (uint32_t k = threadIdx.x; k < nm; k += 1024) kbase[k] = P.bvh_keybase[k];
   __syncthreads();
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co) {
+  tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f) {
     trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhLds{nodes, lds_tris, entries, kbase},
-                                     nullptr, co);
+                                     nullptr, co, f);
   });
 }
 
@@ -2079,7 +2086,9 @@ static hipError_t prepare_schedule(TraceParams& q, hipStream_t stream) {
     if ((e = hipMemsetAsync(q.sched + 8, 0, 192 * 4, stream)) != hipSuccess) return e;  // histogram, cursors
     plan_hist<<<(tiles + 255) / 256, 256, 0, stream>>>(q.sched, q.tile_cost, tiles);
     // factor auto (-1): 3 when a resident wave gets more than 4 tiles, else 1 (profiles/r01k_schedule_sweep)
-    const uint32_t waves = q.num_cus * 16u;
+    // a launch of nf frames: a resident wave's fair share is nf frames' work, i.e. waves / nf per frame
+    const uint32_t nf = q.n_frames > 1 ? q.n_frames : 1u;
+    const uint32_t waves = std::max(1u, q.num_cus * 16u / nf);
     const uint32_t factor = q.split_factor >= 0 ? (uint32_t)q.split_factor : tiles > 4 * waves ? 3u : 1u;
     plan_scan<<<1, 64, 0, stream>>>(q.sched, waves, factor, q.split_k, q.split_prio);
     plan_fill<<<(tiles + 255) / 256, 256, 0, stream>>>(q.sched, q.tile_cost, tiles, q.split_k, q.split_prio,
@@ -2146,7 +2155,8 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
       // resident wave gets more than 6 tiles (the full frame), else 3 (row partitions at N > 1)
       // (profiles/r01o_lane_weighted_sum_factor_sweep.jsonl)
       if (q.split_k == 0) q.split_k = 8;
-      if (q.split_factor < 0) q.split_factor = tiles_of(p) > 6 * p.num_cus * 16u ? 2 : 3;
+      if (q.split_factor < 0)
+        q.split_factor = (uint64_t)tiles_of(p) * std::max(1u, p.n_frames) > 6ull * p.num_cus * 16u ? 2 : 3;
       const size_t lds = wq_lds_bytes(p, &q.wq_ncap, &q.wq_tcap);
       if (p.wq_ncap) q.wq_ncap = std::min(q.wq_ncap, std::max(128u, p.wq_ncap & ~63u));  // HRT_OPT_WQ_NODE_CAP
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;

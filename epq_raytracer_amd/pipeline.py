@@ -162,6 +162,10 @@ class HrtContext:
     def accumulate(self, frame: int):
         self._check(self.lib.hrt_accumulate(self.handle, int(frame) & 0xFFFFFFFF), "hrt_accumulate")
 
+    def compute_n(self, pc: _lib.PushConstants, n: int):
+        """hrt_compute_n: n x (trace with rng_offset = pc.rng_offset + k, accumulate(that k))."""
+        self._check(self.lib.hrt_compute_n(self.handle, ctypes.byref(pc), int(n)), "hrt_compute_n")
+
     def synchronize(self):
         self._check(self.lib.hrt_synchronize(self.handle), "hrt_synchronize")
 

@@ -210,7 +210,10 @@ typedef enum hrt_option {
   /* persistent kernels: the first trace of a context (no previous tile costs) is preceded by a
    * 1-sample probe trace into a scratch image whose per-tile costs plan it (1 default, 0 off).
    * Frames, counters and the trace timing are unaffected. */
-  HRT_OPT_PROBE = 11
+  HRT_OPT_PROBE = 11,
+  /* hrt_compute_n: frames traced by one persistent launch (default 16, 1 = one launch per frame;
+   * also capped at 1 GiB of frame images).  Results do not depend on it. */
+  HRT_OPT_FRAMES_PER_LAUNCH = 12
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */
@@ -269,6 +272,15 @@ hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc);
 
 /* One dispatch of image_combiner.glsl with next_image = this context's trace image. */
 hrt_status hrt_accumulate(hrt_context* ctx, uint32_t frame);
+
+/* The frame loop of compute_n_then_render (src/raytracing_app.rs:198-227, without the present):
+ * for k = pc->rng_offset .. pc->rng_offset + n - 1, one trace of pc with rng_offset = k followed by
+ * hrt_accumulate(ctx, k) -- byte for byte the result of that loop of hrt_trace / hrt_accumulate
+ * calls, the trace image holding the last frame afterwards.  The persistent kernels trace up to
+ * HRT_OPT_FRAMES_PER_LAUNCH frames in one launch (each frame its own image), so that the long
+ * per-pixel sample chains of one frame run beside the other frames' work instead of ending each
+ * frame alone; the combiner then folds the frames in order.  pc->init must be 0. */
+hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* pc, uint32_t n);
 
 /* Copy this context's local rows of an image (row-major, local_rows x width x 4 channels) into dst,
  * which may be host or device memory.  Blocking.  bytes must be >= the image size in fmt. */

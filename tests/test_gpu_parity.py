@@ -274,6 +274,58 @@ def test_progressive_accumulation_matches_oracle(mode):
         np.testing.assert_array_equal(got.view(np.uint32), acc.view(np.uint32))
 
 
+@pytest.mark.parametrize("fpl", [1, 3, 16])
+@pytest.mark.parametrize("scene,size,spp,variant,mode,partition", [
+    ("island", (96, 64), 3, 9, _lib.MODE_RGBA8, None),
+    ("island", (96, 64), 3, 7, _lib.MODE_RGBA8, None),
+    ("island", (96, 64), 3, 8, _lib.MODE_RGBA32F, None),
+    ("cave", (64, 48), 2, 0, _lib.MODE_RGBA32F, None),
+    ("box", (45, 33), 3, 5, _lib.MODE_RGBA8, None),          # not persistent: one launch per frame
+    ("island", (256, 256), 1, 0, _lib.MODE_RGBA8, None),     # 1024 tiles: probe-planned first launch
+    ("island", (80, 70), 2, 9, _lib.MODE_RGBA8, (8, 1, 3)),  # a row-tile partition
+])
+def test_compute_n_matches_frame_loop(scene, size, spp, variant, mode, partition, fpl):
+    """hrt_compute_n (compute_n_then_render's loop, src/raytracing_app.rs:198-227): up to
+    HRT_OPT_FRAMES_PER_LAUNCH frames per persistent launch, each frame its own image, the combiner
+    folding them in order -- byte for byte the per-frame hrt_trace / hrt_accumulate loop (accumulator,
+    last trace image, counters), for 7 frames from rng_offset 3 (launches of 3 + 2 + 2 at fpl 3)."""
+    case = SceneCase(scene, size, spp, 8)
+    first, n = 3, 7
+    fmt = _lib.FMT_RGBA8 if mode == _lib.MODE_RGBA8 else _lib.FMT_RGBA32F
+    loop = case.context(mode=mode, variant=variant, partition=partition)
+    for k in range(first, first + n):
+        loop.trace(case.push(k))
+        loop.accumulate(k)
+    a = loop.stats()
+    want_acc, want_trace = loop.read(_lib.IMG_ACCUM, fmt), loop.read(_lib.IMG_TRACE, fmt)
+    loop.close()
+    ctx = case.context(mode=mode, variant=variant, partition=partition,
+                       options={_lib.OPT_FRAMES_PER_LAUNCH: fpl})
+    ctx.compute_n(case.push(first), n)
+    b = ctx.stats()
+    got_acc, got_trace = ctx.read(_lib.IMG_ACCUM, fmt), ctx.read(_lib.IMG_TRACE, fmt)
+    ctx.compute_n(case.push(first + n), 2)  # a planned launch after a batched one
+    ctx.synchronize()
+    ctx.close()
+    assert np.array_equal(got_trace.view(np.uint8), want_trace.view(np.uint8))
+    assert np.array_equal(got_acc.view(np.uint8), want_acc.view(np.uint8))
+    assert (b.segments, b.tri_tests, b.traces, b.accumulates) == (a.segments, a.tri_tests, a.traces, a.accumulates)
+    assert b.last_kernel == a.last_kernel
+
+
+def test_compute_n_arguments():
+    case = SceneCase("box", (16, 16), 1, 2)
+    ctx = case.context()
+    with pytest.raises(_lib.HrtError):
+        ctx.compute_n(case.push(1, init=True), 2)
+    for bad in (0, 1025):
+        with pytest.raises(_lib.HrtError):
+            ctx.set_option(_lib.OPT_FRAMES_PER_LAUNCH, bad)
+    ctx.compute_n(case.push(1), 0)  # no frames: nothing to do
+    assert ctx.stats().traces == 0
+    ctx.close()
+
+
 @pytest.mark.parametrize("parts,tile", [(2, 16), (3, 16), (8, 4)])
 def test_row_tile_partition_reassembles_full_frame(parts, tile):
     from epq_raytracer_amd import rowtiles

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--ncap", type=int, default=0)
     ap.add_argument("--probe", type=int, default=1)
     ap.add_argument("--sec-batch", type=int, default=48)
+    ap.add_argument("--batch", type=int, default=0,
+                    help="> 0: each measurement is hrt_compute_n of this many frames (ms = per frame, wall incl. accumulates)")
     a = ap.parse_args()
     W, H = (int(v) for v in a.size.split("x"))
     case = SceneCase(a.scene, (W, H), a.spp, a.bounces)
@@ -39,12 +41,24 @@ def main():
                                 _lib.OPT_WQ_NODE_CAP: a.ncap, _lib.OPT_PROBE: a.probe})
     pc = case.push(1)
     ms = []
-    for _ in range(a.frames):
+    if a.batch > 0:
+        import time
+        ctx.set_option(_lib.OPT_FRAMES_PER_LAUNCH, a.batch)
+        k = 1
+        for _ in range(a.frames):
+            ctx.synchronize()
+            ctx.reset_stats()
+            t0 = time.perf_counter()
+            ctx.compute_n(case.push(k), a.batch)
+            ctx.synchronize()
+            ms.append(round((time.perf_counter() - t0) * 1e3 / a.batch, 3))
+            k += a.batch
+    for _ in range(a.frames if a.batch <= 0 else 0):
         ctx.reset_stats()
         ctx.trace(pc)
         ms.append(round(ctx.stats().total_trace_ms, 3))
     ctx.close()
-    print(json.dumps({"scene": a.scene, "variant": a.variant, "partition": a.partition, "coop": a.coop, "factor": a.factor,
+    print(json.dumps({"batch": a.batch, "scene": a.scene, "variant": a.variant, "partition": a.partition, "coop": a.coop, "factor": a.factor,
                       "split": a.split, "sec_batch": a.sec_batch, "ncap": a.ncap, "probe": a.probe, "ms": ms}))
 
 
