@@ -70,7 +70,7 @@ struct hrt_context {
   uint32_t coop = 1;      // HRT_OPT_COOP
   uint32_t wq_node_cap = 0;  // HRT_OPT_WQ_NODE_CAP (0 = auto)
   uint32_t probe = 1;        // HRT_OPT_PROBE
-  uint32_t frames_per_launch = 16;  // HRT_OPT_FRAMES_PER_LAUNCH (hrt_compute_n)
+  uint32_t frames_per_launch = 64;  // HRT_OPT_FRAMES_PER_LAUNCH (hrt_compute_n)
   void* frame_stack = nullptr;      // hrt_compute_n: frame_stack_frames trace images
   uint32_t frame_stack_frames = 0;
   uint32_t num_cus = 0;
@@ -95,7 +95,7 @@ struct hrt_context {
   int variant = 0;
   bool counters_on = true;
   bool diag_on = false;
-  uint32_t sec_batch = 48;
+  uint32_t sec_batch = 0;  // HRT_OPT_SECONDARY_BATCH (0 = auto per kernel, launch_trace)
   int last_kernel = 0, last_block = 0;  // what the last hrt_trace launched (hrt_stats)
 
   struct Import {
@@ -820,7 +820,8 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       ctx->diag_on = value == 2;
       return HRT_OK;
     case HRT_OPT_SECONDARY_BATCH:
-      if (value < 1 || value > 64) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "secondary batch must be in [1, 64]");
+      if (value < 0 || value > 64)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "secondary batch must be 0 (auto) or in [1, 64]");
       ctx->sec_batch = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_SPLIT:

@@ -2099,7 +2099,8 @@ static hipError_t prepare_schedule(TraceParams& q, hipStream_t stream) {
   return hipMemsetAsync(q.sched, 0, 4, stream);
 }
 
-hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, int* ran, int* block_out) {
+hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, int* ran, int* block_out) {
+  TraceParams p = p0;
   static bool lds_attr = false;
   if (!lds_attr) {
     lds_attr = true;
@@ -2121,6 +2122,10 @@ hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, i
   }
   variant = resolve_variant(p, variant);
   *ran = variant;
+  // bounce batch threshold, auto: the pair traversal's step cost scales with its rays, so BUNDLE_WQ
+  // batches earlier (28 of 64 lanes); the cull kernels test every survivor for the whole wave (48)
+  // (profiles/r01q_sec_batch_sweep.jsonl, frames in 16-frame launches)
+  if (p.sec_batch == 0) p.sec_batch = variant == HRT_KERNEL_BUNDLE_WQ ? 28u : 48u;
   *block_out = variant == HRT_KERNEL_BRUTE_LDS ? 1024 : 256;
   const dim3 grid((p.pc.width + 15) / 16, (p.local_rows + 15) / 16, 1);
   switch (variant) {

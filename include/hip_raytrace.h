@@ -182,7 +182,8 @@ typedef enum hrt_option {
    * kernels' cull diagnostics (hrt_get_diagnostics) */
   HRT_OPT_COUNTERS = 2,
   /* bundle kernel: a wave runs its bounce (non-primary) segments once this many lanes wait for one,
-   * or when no lane has a primary segment left (1..64, default 48; results do not depend on it) */
+   * or when no lane has a primary segment left (1..64; default 0 = auto: 28 for BUNDLE_WQ, else 48;
+   * results do not depend on it) */
   HRT_OPT_SECONDARY_BATCH = 3,
   /* BUNDLE_BVH: triangles per leaf of the hierarchy the next hrt_set_scene builds (1..16, default 4) */
   HRT_OPT_BVH_LEAF_SIZE = 4,
@@ -211,7 +212,7 @@ typedef enum hrt_option {
    * 1-sample probe trace into a scratch image whose per-tile costs plan it (1 default, 0 off).
    * Frames, counters and the trace timing are unaffected. */
   HRT_OPT_PROBE = 11,
-  /* hrt_compute_n: frames traced by one persistent launch (default 16, 1 = one launch per frame;
+  /* hrt_compute_n: frames traced by one persistent launch (default 64, 1 = one launch per frame;
    * also capped at 1 GiB of frame images).  Results do not depend on it. */
   HRT_OPT_FRAMES_PER_LAUNCH = 12
 } hrt_option;

@@ -313,6 +313,22 @@ def test_compute_n_matches_frame_loop(scene, size, spp, variant, mode, partition
     assert b.last_kernel == a.last_kernel
 
 
+@pytest.mark.parametrize("sec_batch", [0, 1, 28, 64])
+@pytest.mark.parametrize("variant", [5, 7, 9])
+def test_secondary_batch_values(variant, sec_batch):
+    """HRT_OPT_SECONDARY_BATCH (0 = auto: 28 for BUNDLE_WQ, else 48) only changes when a wave runs its
+    waiting bounce segments, never a byte or a count."""
+    case = SceneCase("island", (75, 41), 3, 8)
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context(variant=variant, options={_lib.OPT_SECONDARY_BATCH: sec_batch})
+    ctx.trace(case.push())
+    st = ctx.stats()
+    img = ctx.read(_lib.IMG_TRACE)
+    ctx.close()
+    assert np.array_equal(img, ref), mismatch_report(img, ref)
+    assert (st.segments, st.tri_tests) == (seg, tt)
+
+
 def test_compute_n_arguments():
     case = SceneCase("box", (16, 16), 1, 2)
     ctx = case.context()

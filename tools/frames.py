@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--split", type=int, default=0)
     ap.add_argument("--ncap", type=int, default=0)
     ap.add_argument("--probe", type=int, default=1)
-    ap.add_argument("--sec-batch", type=int, default=48)
+    ap.add_argument("--sec-batch", type=int, default=0)
     ap.add_argument("--batch", type=int, default=0,
                     help="> 0: each measurement is hrt_compute_n of this many frames (ms = per frame, wall incl. accumulates)")
     a = ap.parse_args()

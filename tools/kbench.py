@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--no-ref", action="store_true", help="skip the literal-kernel reference frame")
     ap.add_argument("--diag", action="store_true", help="also print the bundle kernels' cull diagnostics")
-    ap.add_argument("--sec-batch", type=int, nargs="+", default=[48], help="HRT_OPT_SECONDARY_BATCH values to sweep")
+    ap.add_argument("--sec-batch", type=int, nargs="+", default=[0], help="HRT_OPT_SECONDARY_BATCH values to sweep (0 = auto)")
     ap.add_argument("--split", type=int, nargs="+", default=[0], help="HRT_OPT_SPLIT values to sweep (LDS variants)")
     ap.add_argument("--prio", type=int, nargs="+", default=[1], help="HRT_OPT_PRIORITY values to sweep")
     ap.add_argument("--factor", type=int, nargs="+", default=[-1], help="HRT_OPT_SPLIT_FACTOR values to sweep")
