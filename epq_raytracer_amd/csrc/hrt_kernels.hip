@@ -587,7 +587,36 @@ struct TileList {
   uint32_t* lds;   // LDS list (nullptr: VGPR list)
   uint32_t n;
   bool ok;
+  // aabb_pass of every mesh (<= 8) for a ray from cam_pos by the sign octant of its direction:
+  // bit 8m + (sx | sy << 1 | sz << 2) (aabb_truth_table); aabb_ok false -> the literal test
+  unsigned long long aabb;
+  bool aabb_ok;
 };
+
+// intersecting_aabb's result for origin o depends only on the signs of (bound - o) and of 1/d per
+// axis, as long as no product (bound - o) * (1/d) is zero or NaN: each "> 0" test is then a sign
+// test, and the quirked min/max chain (raytracing.glsl:199-207) reduces to
+//   tx_far > 0 || tx_near > 0 || ty_far > 0 || tz_far > 0 || tz_near > 0.
+// So with every bound - o nonzero and not NaN, and |d| <= 1.5 per component (|1/d| >= 2/3, so a
+// nonzero product cannot round to 0), aabb_pass(m, o, d) == aabb_pass(m, o, (+-1, +-1, +-1)) with
+// d's sign bits (1/+-0 = +-inf keeps the sign).  Lane l evaluates mesh l >> 3 at octant l & 7.
+__device__ __forceinline__ void aabb_truth_table(const TraceParams& P, TileList& t) {
+  const hrt_push_constants& pc = P.pc;
+  const uint32_t lane = threadIdx.x & 63, m = lane >> 3, oct = lane & 7;
+  const f3 o = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
+  bool pass = false, bad = false;
+  if (m < (uint32_t)pc.num_meshes) {
+    const hrt_mesh& mesh = P.meshes[m];
+    for (int a = 0; a < 3; ++a) {
+      const float ov = a == 0 ? o.x : (a == 1 ? o.y : o.z);
+      const float lo = mesh.min_point[a] - ov, hi = mesh.max_point[a] - ov;
+      bad |= !(lo < 0.0f || lo > 0.0f) || !(hi < 0.0f || hi > 0.0f);  // zero or NaN
+    }
+    pass = aabb_pass(mesh, o, mk((oct & 1) ? -1.0f : 1.0f, (oct & 2) ? -1.0f : 1.0f, (oct & 4) ? -1.0f : 1.0f));
+  }
+  t.aabb = __ballot(pass);
+  t.aabb_ok = pc.num_meshes <= 8 && !__any(bad);
+}
 
 __device__ __forceinline__ Bundle tile_bundle(const hrt_push_constants& pc, bool active, f3 centre, bool& ok) {
   const float inf = __builtin_inff();
@@ -626,12 +655,15 @@ __device__ __forceinline__ bool bundle_keep(const float4* __restrict__ cr, uint3
 // Builds the wave's list (all 64 lanes active; the caller synchronises before reading it).
 __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool active, f3 centre, uint32_t* lds) {
   const hrt_push_constants& pc = P.pc;
-  TileList t{0u, lds, 0u, false};
+  TileList t{0u, lds, 0u, false, 0ull, false};
   const uint32_t cap = lds ? kTileCapLds : kTileCapVgpr;
   if (pc.num_meshes > 32 || !__any(active)) return t;
   bool ok;
   const Bundle b = tile_bundle(pc, active, centre, ok);
   if (!ok) return t;
+#ifndef HRT_AABB_LITERAL
+  aabb_truth_table(P, t);
+#endif
   const uint32_t lane = threadIdx.x & 63;
   for (int m = 0; m < pc.num_meshes; ++m) {
     const uint32_t k0 = P.cam_start[m], k1 = k0 + P.cam_count[m];
@@ -668,7 +700,18 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
   const hrt_push_constants& pc = P.pc;
   spheres_first(sc, pc, prim, o, d, c);
   uint32_t pass_mask = 0;
-  if (prim) {
+  // primary lanes start at cam_pos (the table's origin)
+  const bool octant = tl.aabb_ok && fabsf(d.x) <= 1.5f && fabsf(d.y) <= 1.5f && fabsf(d.z) <= 1.5f;
+  if (prim && octant) {
+    const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
+    const unsigned long long row = tl.aabb >> oct;
+    for (int m = 0; m < pc.num_meshes; ++m) {
+      if ((row >> (8 * m)) & 1ull) {
+        pass_mask |= 1u << m;
+        tests += sc.meshes[m].len;
+      }
+    }
+  } else if (prim) {
     for (int m = 0; m < pc.num_meshes; ++m) {
       if (aabb_pass(sc.meshes[m], o, d)) {
         pass_mask |= 1u << m;
@@ -1454,6 +1497,17 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 // segments take the bundle path; a lane whose next segment is a bounce waits (state untouched) until
 // at least sec_batch lanes wait or no primary segment is left in the wave, then all waiting lanes run
 // their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
+#ifdef HRT_EXP_TWICE
+// Timing experiments only (frames unchanged): run one phase a second time on opaque copies of its
+// inputs and discard the result, so the time difference is that phase's marginal cost.
+__device__ __forceinline__ float exp_zero() {
+  float z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
+__device__ __forceinline__ void exp_use(float v) { asm volatile("; use %0" ::"v"(v)); }
+#endif
+
 enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2, kBounceWq = 3 };
 
 template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
@@ -1492,6 +1546,13 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
       } else {
         ++sample;
         const f3 dir = get_ray_dir(pc, centre, state);
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 2
+        {
+          uint32_t s2 = state + (uint32_t)exp_zero();
+          const f3 d2 = normalize(get_ray_dir(pc, centre, s2));
+          exp_use(d2.x + d2.y + d2.z);
+        }
+#endif
         p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, normalize(dir), 0, true};
       }
     }
@@ -1513,6 +1574,15 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (any_prim) {
       if (tl.ok) {
         world_hit_tile(sc, P, tl, prim, p.pos, p.dir, tests, c);
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 1
+        {
+          const float z = exp_zero();
+          Closest c2{kFltMax, 0, 0u, 0u};
+          uint32_t t2 = 0;
+          world_hit_tile(sc, P, tl, prim, p.pos, mk(p.dir.x + z, p.dir.y + z, p.dir.z + z), t2, c2);
+          exp_use(c2.t + (float)t2 + (float)c2.idx);
+        }
+#endif
         if (D && P.diag) {
           dg.prim_considered += tl.n;
           dg.prim_survivors += tl.n;
@@ -1536,6 +1606,15 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (D && P.diag) t2 = __builtin_readcyclecounter();
     if (prim || sec) {
       ++segs;
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 3
+      {
+        Path p2 = p;
+        p2.dir.x = p2.dir.x + exp_zero();
+        uint32_t s2 = state + (uint32_t)exp_zero();
+        exp_use((shade_step(sc, pc, p2, c, s2) ? 1.0f : 0.0f) + p2.dir.x + p2.dir.y + p2.dir.z + p2.light.x +
+                p2.colour.y);
+      }
+#endif
       const bool ended = shade_step(sc, pc, p, c, state);
       ++p.bounce;
       if (ended || p.bounce > pc.max_bounces) {

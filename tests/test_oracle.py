@@ -122,6 +122,38 @@ def test_intersecting_aabb_quirks():
     assert not O.intersecting_aabb([1, 1, 1], [2, 2, 2], [3, 3, 3], [0.0, 1.0, 1.0])
 
 
+def _octant_pass(mn, mx, o, d):
+    """The kernels' primary-ray AABB shortcut (hrt_kernels.hip aabb_truth_table): the reference's
+    quirked test evaluated at the direction's sign octant (+-1 per axis) instead of d itself."""
+    sd = [(-1.0 if math.copysign(1.0, float(v)) < 0 else 1.0) for v in np.float32(d)]
+    return O.intersecting_aabb(mn, mx, o, sd)
+
+
+def test_aabb_octant_rule_matches_quirked_test():
+    # valid while every bound - o is nonzero and not NaN and |d| <= 1.5 per component
+    rng = np.random.default_rng(7)
+    specials = np.float32([0.0, -0.0, 1e-30, -1e-30, 1e-45, -1e-45, 1.0, -1.0, 1.5, -1.5, 1e-7, -1e-7])
+    n = 0
+    for i in range(6000):
+        o = rng.uniform(-20, 20, 3).astype(np.float32)
+        a, b = rng.uniform(-20, 20, 3).astype(np.float32), rng.uniform(-20, 20, 3).astype(np.float32)
+        if i % 7 == 0:  # bounds one ulp off the origin
+            a = np.nextafter(o, np.float32(np.inf)).astype(np.float32)
+        if i % 11 == 0:
+            b = np.nextafter(o, np.float32(-np.inf)).astype(np.float32)
+        mn, mx = np.minimum(a, b), np.maximum(a, b)
+        d = rng.normal(size=3).astype(np.float32)
+        d = (d / np.float32(np.sqrt(np.float32(d @ d)))).astype(np.float32)
+        if i % 3 == 0:
+            d[rng.integers(0, 3)] = specials[rng.integers(0, len(specials))]
+        if i % 5 == 0:
+            d = rng.choice(specials, 3)
+        assert np.all(mn - o != 0) and np.all(mx - o != 0)
+        assert O.intersecting_aabb(mn, mx, o, d) == _octant_pass(mn, mx, o, d), (mn, mx, o, d)
+        n += 1
+    assert n == 6000
+
+
 def test_accumulate_semantics():
     new = np.full((2, 3, 4), 200, np.uint8)
     cur = np.full((2, 3, 4), 77, np.uint8)
