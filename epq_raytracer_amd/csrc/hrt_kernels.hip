@@ -222,22 +222,34 @@ __device__ __forceinline__ void store_pixel(const TraceParams& P, uint32_t x, ui
   if (P.img32) P.img32[idx] = make_float4(col.x, col.y, col.z, 1.0f);
 }
 
-// wave-level sums of the per-lane counters (+ the wave's longest lane), one atomic each per wave.
-__device__ __forceinline__ void flush_counters(const TraceParams& P, uint32_t segs, uint32_t tests) {
-  if (!P.counters) return;
-  unsigned long long s = segs, t = tests;
-  uint32_t mx = segs;
+// wave-level sums of the per-lane counters (+ the wave's longest lane), in every lane.
+__device__ __forceinline__ void wave_counters(uint32_t segs, uint32_t tests, unsigned long long& s,
+                                              unsigned long long& t, uint32_t& mx) {
+  s = segs;
+  t = tests;
+  mx = segs;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     s += __shfl_xor(s, off, 64);
     t += __shfl_xor(t, off, 64);
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
   }
-  if ((threadIdx.x & 63) == 0) {
+}
+__device__ __forceinline__ void add_counters(const TraceParams& P, unsigned long long s, unsigned long long t,
+                                             unsigned long long mx) {
+  if (P.counters && (threadIdx.x & 63) == 0) {
     atomicAdd(&P.counters[0], s);
     atomicAdd(&P.counters[1], t);
-    atomicAdd(&P.counters[2], (unsigned long long)mx);
+    atomicAdd(&P.counters[2], mx);
   }
+}
+// one atomic each per wave
+__device__ __forceinline__ void flush_counters(const TraceParams& P, uint32_t segs, uint32_t tests) {
+  if (!P.counters) return;
+  unsigned long long s, t;
+  uint32_t mx;
+  wave_counters(segs, tests, s, t, mx);
+  add_counters(P, s, t, mx);
 }
 
 __device__ __forceinline__ void lane_pixel(const TraceParams& P, uint32_t& x, uint32_t& lr) {
@@ -824,6 +836,11 @@ struct Coop {
   unsigned long long* ex;        // 3 x 64 slots (LDS)
   uint32_t round;
   uint32_t work;                 // this wave's share of the tile's work units (the planner's cost)
+  // persistent loops: the wave sums its items' counters here and flushes them once at the end
+  // (three same-address global atomics per item serialised in L2: ~40 ns per item, the floor of
+  // low-spp frames -- 4K 4 spp took 5.1 ms per frame)
+  bool defer = false;
+  unsigned long long acc_s = 0, acc_t = 0, acc_m = 0;
 };
 
 __device__ __forceinline__ void coop_merge(Coop& co, Closest& c) {
@@ -1531,6 +1548,13 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   }
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
   const TileList tl = build_tile_list(P, active, centre, list_lds);
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 4
+  {
+    const float z = exp_zero();
+    const TileList t2 = build_tile_list(P, active, mk(centre.x + z, centre.y, centre.z), nullptr);
+    exp_use((float)t2.n + (float)t2.v + (float)t2.aabb);
+  }
+#endif
   // bounce batch threshold scaled to the item's active lanes (a split tile's row group has 8/k rows):
   // a batch of few lanes then runs alongside the other lanes' primary segments instead of after them
   const uint32_t sec_thresh = max(1u, (P.sec_batch * (uint32_t)__popcll(__ballot(active)) + 63u) / 64u);
@@ -1634,7 +1658,16 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     colour = colour / (float)pc.num_samples;
     store_pixel(P, x, lr, colour, frame);
   }
-  flush_counters(P, segs, tests);
+  if (co.defer) {
+    unsigned long long s, t;
+    uint32_t mx;
+    wave_counters(segs, tests, s, t, mx);
+    co.acc_s += s;
+    co.acc_t += t;
+    co.acc_m += mx;
+  } else {
+    flush_counters(P, segs, tests);
+  }
   if (D && P.tile_cycles && (threadIdx.x & 63) == 0) {  // lane 0 sits at the tile's (0, 0)
     const uint32_t tiles_x = (pc.width + 7) / 8;
     unsigned long long* rec = P.tile_cycles + 4 * ((lr / 8) * tiles_x + x / 8);
@@ -1788,20 +1821,32 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
   // let the compiler thread lanes 1-63 straight back to the body past the head, where they spun on
   // a stale item: keep it this way.
   Coop solo{0u, 1u, nullptr, 0u, 0u};
+  solo.defer = true;
   uint32_t prev_tile = 0xFFFFFFFFu, prev_cost = 0, prev_lk = 0;
+  // Items are taken kGrab at a time while far from the end (one same-address atomic per kGrab items;
+  // the plan's longest-first order is kept, and the last 16 x kGrab items per resident wave go singly).
+  // The threshold sum of the planner (sched[6]) is summed per wave and added once.
+  constexpr uint32_t kGrab = 4;
+  const uint32_t resident = gridDim.x * (BLOCK / 64);
+  uint32_t cur = first, end = first;
+  unsigned long long cost_sum = 0;
   for (;;) {
+    const bool refill = cur >= end;  // wave-uniform
+    const uint32_t g = (uint64_t)cur + 16ull * kGrab * resident < n ? kGrab : 1u;
     uint32_t t = 0;
     if (lane == 0) {
-      if (prev_tile != 0xFFFFFFFFu) {
-        // a tile's cost: its items' summed clocks; the heavy threshold's sum counts an item by its
-        // share of the tile's lanes (its work), so splitting does not raise the threshold (with summed
-        // clocks there too, borderline tiles flipped between split and whole: 7.4 / 8.4 ms frames)
-        atomicAdd(&P.tile_cost[prev_tile], prev_cost);
-        atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)(prev_cost >> prev_lk));
-      }
-      t = first + atomicAdd(&P.sched[0], 1u);
+      // a tile's cost: its items' summed clocks; the heavy threshold's sum counts an item by its
+      // share of the tile's lanes (its work), so splitting does not raise the threshold (with summed
+      // clocks there too, borderline tiles flipped between split and whole: 7.4 / 8.4 ms frames)
+      if (prev_tile != 0xFFFFFFFFu) atomicAdd(&P.tile_cost[prev_tile], prev_cost);
+      if (refill) t = first + atomicAdd(&P.sched[0], g);
     }
-    t = __builtin_amdgcn_readfirstlane(t);
+    if (prev_tile != 0xFFFFFFFFu) cost_sum += prev_cost >> prev_lk;
+    if (refill) {
+      cur = __builtin_amdgcn_readfirstlane(t);
+      end = cur + g;
+    }
+    t = cur++;
     if (t >= n) break;
     const uint32_t ti = t / nf, tf = t - ti * nf;
     const uint32_t item = P.items ? __builtin_amdgcn_readfirstlane(P.items[ti]) : 0u;
@@ -1822,10 +1867,10 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     prev_tile = tile;
     prev_lk = lk;
   }
-  if (lane == 0 && prev_tile != 0xFFFFFFFFu) {
-    atomicAdd(&P.tile_cost[prev_tile], prev_cost);
-    atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), (unsigned long long)(prev_cost >> prev_lk));
-  }
+  if (lane == 0 && prev_tile != 0xFFFFFFFFu) atomicAdd(&P.tile_cost[prev_tile], prev_cost);
+  if (prev_tile != 0xFFFFFFFFu) cost_sum += prev_cost >> prev_lk;
+  if (lane == 0 && cost_sum) atomicAdd(reinterpret_cast<unsigned long long*>(P.sched + 6), cost_sum);
+  add_counters(P, solo.acc_s, solo.acc_t, solo.acc_m);
 }
 
 // Planner (after a trace of an LDS variant, before the next).  Items go in decreasing order of the
