@@ -1826,7 +1826,10 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
   // Items are taken kGrab at a time while far from the end (one same-address atomic per kGrab items;
   // the plan's longest-first order is kept, and the last 16 x kGrab items per resident wave go singly).
   // The threshold sum of the planner (sched[6]) is summed per wave and added once.
-  constexpr uint32_t kGrab = 4;
+#ifndef HRT_GRAB
+#define HRT_GRAB 4u
+#endif
+  constexpr uint32_t kGrab = HRT_GRAB;
   const uint32_t resident = gridDim.x * (BLOCK / 64);
   uint32_t cur = first, end = first;
   unsigned long long cost_sum = 0;
