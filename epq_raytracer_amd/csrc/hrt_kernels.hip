@@ -1285,9 +1285,15 @@ __device__ __forceinline__ void wq_leaf_prim(const TraceParams& P, const WqLds& 
   const float4* pr = P.bvh_prims;
   const float4 A = pr[4 * k], B = pr[4 * k + 1], C = pr[4 * k + 2], N = pr[4 * k + 3];
   const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
-  if (!((mask >> m) & 1ull)) return;  // mesh failed its (quirky) AABB test for this ray
   float dist;
+#ifdef HRT_WQ_MASK_FIRST
+  if (!((mask >> m) & 1ull)) return;  // mesh failed its (quirky) AABB test for this ray
   if (wq_tri_accept(A, B, C, N, o, d, wq_slot_t(wq, r) * kOnePlus, dist)) {
+#else
+  // the mesh filter (its quirky AABB test for this ray) joins the acceptance instead of leaving
+  // first, so the four record loads issue together (one L2 round trip per triangle step, not two)
+  if (wq_tri_accept(A, B, C, N, o, d, wq_slot_t(wq, r) * kOnePlus, dist) && ((mask >> m) & 1ull)) {
+#endif
     const uint32_t id = ((m << 26) | __builtin_bit_cast(uint32_t, C.w)) + 1u;
     atomicMin(&wq.slot[r], ((unsigned long long)__float_as_uint(dist) << 32) | id);
   }
@@ -1618,7 +1624,19 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (D && P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
       if constexpr (Bounce == kBounceWq) {
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 5
+        const Closest c_in = c;
+#endif
         world_hit_bounce_wq<D>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 5
+        {
+          const float z = exp_zero();
+          Closest c2 = c_in;
+          uint32_t t2 = 0;
+          world_hit_bounce_wq<D>(sc, P, bsrc, sec, p.pos, mk(p.dir.x + z, p.dir.y + z, p.dir.z + z), t2, c2, dg);
+          exp_use(c2.t + (float)t2 + (float)c2.idx);
+        }
+#endif
       } else if constexpr (Bounce == kBounceBvh) {
         world_hit_bounce_bvh<D>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
       } else if constexpr (Bounce == kBounceCull) {
