@@ -565,9 +565,8 @@ __device__ __forceinline__ float4 ldk(const kfloat* p, uint32_t i) {  // float4 
 
 // Exact per-lane test of compacted camera-facing record k (ao and num_t precomputed), entered only
 // when some lane has dn < 0.
-__device__ __forceinline__ void primary_exact(const kfloat* ct, uint32_t k, float dn, f3 d, uint32_t m, Closest& c,
-                                              float& best_k) {
-  const float4 A = ldk(ct, 4 * k), B = ldk(ct, 4 * k + 1), C = ldk(ct, 4 * k + 2);
+__device__ __forceinline__ void primary_exact_rec(const float4& A, const float4& B, const float4& C, float dn, f3 d,
+                                                  uint32_t m, Closest& c, float& best_k) {
   TriPre q;
   q.num_t = A.w;
   const f3 dao = cross(mk(A.x, A.y, A.z), d);
@@ -579,6 +578,14 @@ __device__ __forceinline__ void primary_exact(const kfloat* ct, uint32_t k, floa
     if (q.cand) tri_exact(q, __builtin_bit_cast(uint32_t, B.w), m, c, best_k);
   }
 }
+__device__ __forceinline__ void primary_exact(const kfloat* ct, uint32_t k, float dn, f3 d, uint32_t m, Closest& c,
+                                              float& best_k) {
+  primary_exact_rec(ldk(ct, 4 * k), ldk(ct, 4 * k + 1), ldk(ct, 4 * k + 2), dn, d, m, c, best_k);
+}
+// All 64 bytes of camera record k in one scalar load (s_load_dwordx16)
+typedef float kf16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(4))) const kf16 kf16c;
+__device__ __forceinline__ kf16 ld_rec(const kfloat* ct, uint32_t k) { return *(kf16c*)(ct + 16 * (size_t)k); }
 
 // ---- per-wave primary triangle list ------------------------------------------------------------
 // Every primary direction a wave can produce is normalize(M * nc) with nc = centre + (0, t2.y, t1.z),
@@ -739,9 +746,19 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
     const bool pass = (pass_mask >> m) & 1u;
     if (!__any(pass)) continue;
+#ifdef HRT_PRIM_SPLIT_LOADS
     const float4 N = ldk(ct, 4 * kk + 3);
     const float dn = pass ? dot(d, mk(N.x, N.y, N.z)) : 0.0f;
     if (__any(dn < 0.0f)) primary_exact(ct, kk, dn, d, m, c, best_k);
+#else
+    // the whole record in one load: the exact test's operands arrive with the normal (one K$ round
+    // trip per entry instead of two dependent ones)
+    const kf16 R = ld_rec(ct, kk);
+    const float dn = pass ? dot(d, mk(R[12], R[13], R[14])) : 0.0f;
+    if (__any(dn < 0.0f))
+      primary_exact_rec(make_float4(R[0], R[1], R[2], R[3]), make_float4(R[4], R[5], R[6], R[7]),
+                        make_float4(R[8], R[9], R[10], R[11]), dn, d, m, c, best_k);
+#endif
   }
 }
 
