@@ -1006,9 +1006,17 @@ __device__ __forceinline__ void bvh_tri_test(const float4& A, const float4& B, c
 __device__ __forceinline__ void bvh_prim_test(const float4* __restrict__ pr, uint32_t k, unsigned long long mask, f3 o,
                                               f3 d, Closest& c, uint32_t& bkey, float& best_k) {
   const float4 A = pr[4 * k], B = pr[4 * k + 1];
+#ifndef HRT_PRIM_TWO_TRIPS
+  // all four record loads before the mesh filter (one memory round trip per test, not two: the
+  // compiler would otherwise sink C and N below the branch)
+  const float4 C = pr[4 * k + 2], N = pr[4 * k + 3];
+  asm volatile("; record %0 %1" ::"v"(C.x), "v"(N.x));
+#endif
   const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
   if (!((mask >> m) & 1ull)) return;  // mesh failed its (quirky) AABB test for this lane
+#ifdef HRT_PRIM_TWO_TRIPS
   const float4 C = pr[4 * k + 2], N = pr[4 * k + 3];
+#endif
   bvh_tri_test(A, B, C, N, __builtin_bit_cast(uint32_t, A.w), __builtin_bit_cast(uint32_t, C.w), m, o, d, c, bkey,
                best_k);
 }
