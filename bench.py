@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--bounces", type=int, default=8, help="max_bounces")
     ap.add_argument("--variant", type=int, default=0,
                     help="hrt_kernel: 0 auto, 1 literal, 2 brute, 3 brute_lds, 4 bundle, 5 bundle_cull")
-    ap.add_argument("--row-tile", type=int, default=16)
+    ap.add_argument("--row-tile", type=int, default=8)
     ap.add_argument("--frames-per-launch", type=int, default=64,
                     help="> 1: steps run as hrt_compute_n (compute_n_then_render) with up to this many frames per "
                          "trace launch; 1: one trace + accumulate (+ gather) dispatch per step (compute_then_render)")
