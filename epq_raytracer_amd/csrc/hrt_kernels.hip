@@ -1727,7 +1727,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(P.tile_cycles + 4 * ((lr / 8) * tiles_x + x / 8) + 2,
               (unsigned long long)dg.bvh_visits + ((unsigned long long)(dg.bvh_prims + dg.bvh_band) << 32));
   }
-  if (P.diag && (threadIdx.x & 63) == 0) {
+  if (D && P.diag && (threadIdx.x & 63) == 0) {
     atomicAdd(&P.diag[10], (unsigned long long)dg.cyc_prim);
     atomicAdd(&P.diag[11], (unsigned long long)dg.cyc_sec);
     atomicAdd(&P.diag[12], (unsigned long long)dg.cyc_shade);
@@ -1743,7 +1743,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[5], (unsigned long long)dg.sec_survivors);
     atomicAdd(&P.diag[6], (unsigned long long)dg.sec_lanes);
   }
-  if (P.diag && (Bounce == kBounceBvh || Bounce == kBounceWq)) {
+  if (D && P.diag && (Bounce == kBounceBvh || Bounce == kBounceWq)) {
     atomicAdd(&P.diag[7], (unsigned long long)dg.bvh_visits);
     atomicAdd(&P.diag[8], (unsigned long long)dg.bvh_prims);
     atomicAdd(&P.diag[9], (unsigned long long)dg.bvh_band);

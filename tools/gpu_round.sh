@@ -17,7 +17,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-
 find $OUT/prof -name '*kernel_stats.csv' -exec cat {} \;
 timeout -k 10 300 python3 tools/tile_profile.py > $OUT/tile_profile.json 2>&1 || { echo "tile profile failed"; tail -20 $OUT/tile_profile.json; exit 1; }
 timeout -k 10 300 python3 tools/frames.py --frames 8 > $OUT/frames.json 2>&1 || { echo "frames failed"; tail -20 $OUT/frames.json; exit 1; }
-for n in 2 4 8; do timeout -k 10 300 python3 tools/frames.py --frames 6 --partition 16,0,$n >> $OUT/frames.json 2>&1 || { echo "frames failed"; exit 1; }; done
+for n in 2 4 8; do timeout -k 10 300 python3 tools/frames.py --frames 6 --partition 8,0,$n >> $OUT/frames.json 2>&1 || { echo "frames failed"; exit 1; }; done
 cat $OUT/frames.json
 for v in 9 7; do timeout -k 10 300 python3 tools/frames.py --scene cave --variant $v --frames 5 >> $OUT/frames.json 2>&1 || { echo "cave frames failed"; exit 1; }; done
 tail -2 $OUT/frames.json
