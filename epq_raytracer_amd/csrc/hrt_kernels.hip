@@ -1256,9 +1256,8 @@ __device__ __forceinline__ uint32_t wq_escape(const float4* nodes, uint32_t k) {
 // (allowed for in both the back-face bound and the sine bound; cos is rounded down and sin up), and
 // the hardware square root (1 ulp; +2e-7 keeps the sine an upper bound) -- a node is only ever kept
 // more often than by bvh_node_visit.  t_near: the box entry distance (ordering only).
-__device__ __forceinline__ bool wq_node_visit(const float4* nd, f3 o, f3 d, f3 inv, float R, float abs_t, float t_hi,
-                                              float& t_near) {
-  const float4 N0 = nd[0], N1 = nd[1], N2 = nd[2];
+__device__ __forceinline__ bool wq_node_visit_r(const float4& N0, const float4& N1, const float4& N2, f3 o, f3 d,
+                                                f3 inv, float R, float abs_t, float t_hi, float& t_near) {
   const uint32_t w8 = __builtin_bit_cast(uint32_t, N2.x), w9 = __builtin_bit_cast(uint32_t, N2.y),
                  w10 = __builtin_bit_cast(uint32_t, N2.z);
   const float x = half_lo(w8) * d.x + half_hi(w8) * d.y + half_lo(w9) * d.z;
@@ -1273,6 +1272,10 @@ __device__ __forceinline__ bool wq_node_visit(const float4* nd, f3 o, f3 d, f3 i
   const float tf = fminf(fminf(t_hi, fmaxf(tx0, tx1)), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
   t_near = tn;
   return !((tn - fabsf(tn) * 1e-6f) > (tf + fabsf(tf) * 1e-6f));  // NaN -> visit
+}
+__device__ __forceinline__ bool wq_node_visit(const float4* nd, f3 o, f3 d, f3 inv, float R, float abs_t, float t_hi,
+                                              float& t_near) {
+  return wq_node_visit_r(nd[0], nd[1], nd[2], o, d, inv, R, abs_t, t_hi, t_near);
 }
 
 // Exact reference test (raytracing.glsl:213-241) of BVH leaf prim record (a, -) (e1, -) (e2, -) (n, -):
@@ -1467,6 +1470,19 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
           }
         }
         const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
+#ifndef HRT_WQ_NODE_SERIAL
+        if (!deep) {
+          // both children's records read up front (six LDS reads in flight instead of a chain of
+          // dependent reads behind each child's back-face early-out)
+          const float4* na = wq.nodes + 3 * sn[0];
+          const float4* nb = wq.nodes + 3 * sn[1];
+          const float4 A0 = na[0], A1 = na[1], A2 = na[2], B0 = nb[0], B1 = nb[1], B2 = nb[2];
+          si[0] = __builtin_bit_cast(uint32_t, A2.w);
+          si[1] = __builtin_bit_cast(uint32_t, B2.w);
+          sk[0] = wq_node_visit_r(A0, A1, A2, ro, rd, rinv, rR, rabs, t_hi, st[0]);
+          sk[1] = wq_node_visit_r(B0, B1, B2, ro, rd, rinv, rR, rabs, t_hi, st[1]);
+        } else
+#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           if (sv[k]) {
