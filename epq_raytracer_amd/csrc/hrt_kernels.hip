@@ -1078,21 +1078,13 @@ __device__ __forceinline__ bool bvh_node_visit(const float4& N0, const float4& N
 // (component < 0), (u, v) = the two minor components over the major one's magnitude.
 __device__ __forceinline__ uint32_t dir_cell(f3 d, uint32_t res) {
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-  uint32_t face;
-  float u, v;
-  if (ax >= ay && ax >= az) {
-    face = d.x < 0.0f ? 1u : 0u;
-    u = d.y / ax;
-    v = d.z / ax;
-  } else if (ay >= az) {
-    face = d.y < 0.0f ? 3u : 2u;
-    u = d.z / ay;
-    v = d.x / ay;
-  } else {
-    face = d.z < 0.0f ? 5u : 4u;
-    u = d.x / az;
-    v = d.y / az;
-  }
+  // operands selected per lane, then one pair of divides (the same quotients as dividing inside
+  // each face's branch, without a wave running up to three divergent pairs)
+  const bool fx = ax >= ay && ax >= az, fy = !fx && ay >= az;
+  const uint32_t face = fx ? (d.x < 0.0f ? 1u : 0u) : fy ? (d.y < 0.0f ? 3u : 2u) : (d.z < 0.0f ? 5u : 4u);
+  const float den = fx ? ax : fy ? ay : az;
+  const float u = (fx ? d.y : fy ? d.z : d.x) / den;
+  const float v = (fx ? d.z : fy ? d.x : d.y) / den;
   const float s = 0.5f * (float)res;
   const int iu = min((int)res - 1, max(0, (int)((u + 1.0f) * s)));  // NaN converts to 0
   const int iv = min((int)res - 1, max(0, (int)((v + 1.0f) * s)));
