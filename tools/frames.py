@@ -61,7 +61,7 @@ def main():
         ms.append(round(ctx.stats().total_trace_ms, 3))
     ctx.close()
     print(json.dumps({"batch": a.batch, "scene": a.scene, "variant": a.variant, "partition": a.partition, "coop": a.coop, "factor": a.factor,
-                      "split": a.split, "sec_batch": a.sec_batch, "ncap": a.ncap, "probe": a.probe, "leaf": a.leaf, "ms": ms}))
+                      "split": a.split, "sec_batch": a.sec_batch, "ncap": a.ncap, "probe": a.probe, "leaf": a.leaf, "prio": a.prio, "ms": ms}))
 
 
 if __name__ == "__main__":
