@@ -5,8 +5,11 @@ samples per pixel (rng_offset = frame index) + one accumulate.  The K timed step
 of compute_n_then_render (src/raytracing_app.rs:198-227): one hrt_compute_n call of K frames (the
 persistent kernel traces up to --frames-per-launch of them per launch, each frame its own image, the
 combiner folding them in order -- byte for byte the per-frame loop), then, when N > 1, the row-tile
-gather of the accumulated framebuffer for its present.  --frames-per-launch 1 runs the realtime loop
-instead (compute_then_render: trace + accumulate + gather per frame).
+gather of the accumulated framebuffer for its present -- hrt_read_image on a context joined to an RCCL
+communicator (hrt_comm_init: one ncclGather to rank 0 + the row un-interleave on rank 0's device,
+behind the C ABI).  --frames-per-launch 1 runs the realtime loop instead (compute_then_render: trace
++ accumulate + gather per frame); the line also reports per_frame_dispatch_ms, a short realtime loop
+measured after the timed steps.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -37,7 +40,7 @@ BYTES_PER_PIXEL_FRAME = 32  # 16 B ray centre + 4 B trace store + 12 B combiner 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene", default="island")
     ap.add_argument("--width", type=int, default=1920)
@@ -53,7 +56,11 @@ def parse():
     ap.add_argument("--verify", action="store_true",
                     help="N>1: rank 0 re-renders all frames on one full-frame context and compares the gathered frame")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl = RCCL over xGMI (default); gloo = host-staged gather (rehearsal on one GPU)")
+                    help="nccl = the library's RCCL gather over xGMI (default); gloo = torch all-gather of the "
+                         "local blocks through the host (rehearsal with several ranks on one GPU)")
+    ap.add_argument("--realtime-frames", type=int, default=16,
+                    help="after the timed steps: frames of the per-frame dispatch loop (compute_then_render) "
+                         "reported as per_frame_dispatch_ms (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length (0 = skip)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per trace launch for this workload")
@@ -98,12 +105,22 @@ def main():
     diffuse.next_frame(0, raytrace.image())
     frame = 1
 
-    local = torch.empty((ctx.local_rows, W, 4), dtype=torch.uint8, device=coll_dev) if dist_on else None
-    full = None
+    lib_gather = dist_on and not gloo
+    if lib_gather:  # RCCL communicator inside the library: rank 0's id shared through torch.distributed
+        uid = [E.HrtContext.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(uid[0], rank, world)
+    local = torch.empty((ctx.local_rows, W, 4), dtype=torch.uint8, device=coll_dev) if dist_on and gloo else None
+    full = torch.empty((H, W, 4), dtype=torch.uint8, device=f"cuda:{device}") if lib_gather and rank == 0 else None
 
     def present():
         nonlocal full
-        if dist_on:  # the framebuffer gather: one all-gather of equal-size row-tile blocks
+        if lib_gather:  # the framebuffer gather behind the C ABI: one ncclGather + un-interleave on rank 0
+            if rank == 0:
+                ctx.read_into(_lib.IMG_ACCUM, _lib.FMT_RGBA8, full.data_ptr(), full.numel())
+            else:
+                ctx.read_into(_lib.IMG_ACCUM, _lib.FMT_RGBA8, 0, 0)
+        elif dist_on:  # gloo rehearsal: all-gather of the equal-size row-tile blocks through the host
             ctx.read_into(_lib.IMG_ACCUM, _lib.FMT_RGBA8, local.data_ptr(), local.numel())
             full = rowtiles.gather_frame(local, H, args.row_tile)
 
@@ -140,15 +157,33 @@ def main():
 
     st = ctx.stats()
     segs, tests = st.segments, st.tri_tests
+    last_trace = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8) if world == 1 else None
+    gathered = full.cpu().numpy() if (dist_on and rank == 0 and full is not None) else None
+    # the realtime loop (compute_then_render per frame, src/main.rs:41-57): consecutive traces overlap
+    # on the context's two trace lanes; measured after the timed steps, separately reported
+    rt_ms = None
+    if args.realtime_frames > 0 and fpl > 1:
+        saved = fpl
+        fpl = 1
+        if dist_on:
+            dist.barrier()
+        ctx.synchronize()
+        t1 = time.perf_counter()
+        steps(args.realtime_frames)
+        ctx.synchronize()
+        if dist_on:
+            dist.barrier()
+        rt_ms = (time.perf_counter() - t1) * 1e3 / args.realtime_frames
+        fpl = saved
     kern_ms = st.total_trace_ms / max(st.traces, 1)  # per frame (a launch of f frames counts f traces)
     launches = -(-args.steps // fpl) if fpl > 1 else args.steps
-    last_frame = frame - 1
-    last_trace = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8) if rank == 0 and world == 1 else None
+    last_frame = frame - 1 - (args.realtime_frames if rt_ms is not None else 0)
     kernel_sym = _lib.kernel_symbol(st.last_kernel, st.last_block)  # what HRT_KERNEL_AUTO resolved to
     if dist_on:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=coll_dev)
+        t = torch.tensor([elapsed, kern_ms, rt_ms or 0.0], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
+        rt_ms = float(t[2]) if rt_ms is not None else None
         c = torch.tensor([segs, tests], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         segs_all, tests_all = int(c[0]), int(c[1])
@@ -165,37 +200,10 @@ def main():
         algorithmic_tf = FLOP_PER_TEST * tests_per_frame / (kern_ms * 1e-3) / 1e12
         pix_local = ctx.local_rows * W
         algo_bytes = BYTES_PER_PIXEL_FRAME * pix_local + (len(raytrace.tris) * 64 + len(raytrace.meshes) * 80)
-        traffic = None
-        pmc_note = None
-        executed_flops = None
-        basis = "unmeasured (no rocprofv3 PMC record for this kernel and scene)"
-        if os.path.exists(args.pmc_json):
-            with open(args.pmc_json) as f:
-                pmc = json.load(f)
-            wl = pmc.get("workload", {})
-            same_kernel = (wl.get("scene"), pmc.get("kernel")) == (args.scene, kernel_sym)
-            exact = same_kernel and (wl.get("width"), wl.get("height"), wl.get("spp"), wl.get("bounces"),
-                                     wl.get("variant")) == (W, H, args.spp, args.bounces, args.variant)
-            per_test = pmc.get("executed_flops_per_reference_test")
-            if exact and world == 1:
-                traffic = pmc.get("hbm_bytes_per_trace_launch")
-                executed_flops = pmc.get("executed_fp32_flops_per_trace_launch")
-                basis = "executed (rocprofv3 PMC FLOP count per launch / live launch time)"
-            elif same_kernel and per_test:
-                # this rank's launch: the profiled kernel's FLOPs per reference triangle test x its own tests
-                executed_flops = per_test * tests_per_frame
-                if exact and pmc.get("hbm_bytes_per_trace_launch"):
-                    traffic = pmc["hbm_bytes_per_trace_launch"] * ctx.local_rows / H
-                basis = ("executed (rocprofv3 PMC FLOPs per reference test of this kernel on " +
-                         f"{wl.get('scene')} {wl.get('width')}x{wl.get('height')} {wl.get('spp')}spp, x this launch's tests)")
-            if executed_flops:
-                pmc_note = os.path.relpath(args.pmc_json, ROOT)
-        # achieved = FP32 FLOPs the kernel executes per launch (hardware-counted by rocprofv3:
-        # 64 * (2*FMA + MUL + ADD) wave-instructions) / the live launch time.  The reference-equivalent
-        # rate (algorithmic_tflops) can exceed the hardware peak and is never reported as achieved.
-        achieved_tf = executed_flops / (kern_ms * 1e-3) / 1e12 if executed_flops else None
+        roof = pmc_roofline(args, world, kernel_sym, kern_ms, tests_per_frame, ctx.local_rows / H, fpl)
         line = {
-            "metric": "Mrays/s (island.obj 1080p 64spp 8-bounce path-trace segments per second)",
+            "metric": (f"Mrays/s ({args.scene}.obj {W}x{H} {args.spp}spp {args.bounces}-bounce path-trace segments "
+                       "per second)"),
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -215,17 +223,15 @@ def main():
                                       f"(trace + accumulate{' + row-tile gather' if dist_on else ''} per frame)"),
                        "frames_per_launch": fpl if fpl > 1 else 1,
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
-                       "parallelism": (f"row-tiles{world}x{args.row_tile} ({args.dist_backend} gather)"
-                                       if dist_on else "single-gpu"),
+                       "parallelism": (f"row-tiles{world}x{args.row_tile} (" +
+                                       ("RCCL ncclGather behind hrt_read_image" if lib_gather else "gloo all-gather")
+                                       + ")" if dist_on else "single-gpu"),
                        "kernel_variant": _lib.KERNEL_NAMES[args.variant]},
             "segments_per_step": segs_all // args.steps,
             "tri_tests_per_step": tests_all // args.steps,
             "paths_per_s": W * H * args.spp / (elapsed / args.steps),
-            "roofline": {"bound": "valu-fp32",
-                         "achieved": round(achieved_tf, 3) if achieved_tf is not None else None,
-                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4) if achieved_tf is not None else None,
-                         "traffic": traffic, "achieved_basis": basis,
+            "per_frame_dispatch_ms": round(rt_ms, 3) if rt_ms is not None else None,
+            "roofline": {"bound": "valu-fp32", **roof,
                          "algorithmic_tflops": round(algorithmic_tf, 3),
                          "kernel": kernel_sym,
                          "kernel_ms": round(kern_ms, 3),
@@ -233,21 +239,71 @@ def main():
                          "kernel_ms_basis": "per frame: launch time / frames per launch (HIP events on the "
                                             "context's stream)",
                          "flop_per_test": FLOP_PER_TEST,
-                         "tests_per_frame": int(tests_per_frame), "pmc_source": pmc_note},
-            "hbm_roofline": {"achieved": round(algo_bytes / (kern_ms * 1e-3) / 1e9, 3), "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": round(algo_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 7),
-                             "algorithmic_bytes_per_frame": algo_bytes, "traffic": traffic},
+                         "tests_per_frame": int(tests_per_frame), "build_id": _lib.build_id()},
+            # BASELINE.md's %HBM-roofline: rocprofv3 counter bytes (FETCH_SIZE x2 + WRITE_SIZE) per frame /
+            # the live per-frame kernel time / 8 TB/s; the compulsory (algorithmic) bytes beside it
+            "hbm_roofline": {"achieved": (round(roof["traffic"] / (kern_ms * 1e-3) / 1e9, 3)
+                                          if roof["traffic"] else None),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": (round(roof["traffic"] / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                                      if roof["traffic"] else None),
+                             "basis": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per frame / live kernel time per frame",
+                             "traffic_per_frame": roof["traffic"],
+                             "algorithmic_bytes_per_frame": algo_bytes,
+                             "algorithmic_gbs": round(algo_bytes / (kern_ms * 1e-3) / 1e9, 3),
+                             "traffic_over_algorithmic": (round(roof["traffic"] / algo_bytes, 2)
+                                                          if roof["traffic"] else None)},
         }
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"], line["parity_sample"] = cpu_baseline(args, raytrace, camera, last_frame,
                                                                        last_trace)
         if dist_on and args.verify:
-            line["gather_check"] = verify_gather(args, full, settings, camera, device, frame - 1)
+            line["gather_check"] = verify_gather(args, gathered, settings, camera, device, last_frame)
         print(json.dumps(line), flush=True)
 
     ctx.close()
     if dist_on:
         dist.destroy_process_group()
+
+
+def pmc_roofline(args, world, kernel_sym, kern_ms, tests_per_frame, row_frac, fpl):
+    """roofline.achieved / frac / traffic from the committed rocprofv3 PMC record of THIS build
+    (profiles/pmc_traffic.json, tools/pmc.sh): executed FP32 FLOP per frame / the live per-frame
+    kernel time.  A record of another build (hrt_build_id), kernel or workload gives null."""
+    from epq_raytracer_amd import _lib
+    out = {"achieved": None, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": None, "traffic": None,
+           "achieved_basis": "unmeasured (no rocprofv3 PMC record of this build, kernel and workload)",
+           "pmc_source": None}
+    if not os.path.exists(args.pmc_json):
+        return out
+    with open(args.pmc_json) as f:
+        pmc = json.load(f)
+    wl = pmc.get("workload", {})
+    want = {"scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
+            "bounces": args.bounces, "kernel_variant": _lib.KERNEL_NAMES[args.variant], "frames_per_launch": fpl}
+    if pmc.get("build_id") != _lib.build_id():
+        out["achieved_basis"] = (f"unmeasured: the PMC record is of build {pmc.get('build_id')}, this library is "
+                                 f"{_lib.build_id()}")
+        return out
+    if pmc.get("kernel") != kernel_sym or any(wl.get(k) != v for k, v in want.items()):
+        out["achieved_basis"] = "unmeasured: the PMC record is of another kernel or workload"
+        return out
+    flops = pmc.get("executed_fp32_flops_per_frame")
+    traffic = pmc.get("hbm_bytes_per_frame")
+    if world > 1:  # this rank's rows: the record's FLOPs per reference test x the rank's own tests
+        per_test = pmc.get("executed_flops_per_reference_test")
+        flops = per_test * tests_per_frame if per_test else None
+        traffic = traffic * row_frac if traffic else None
+    if flops:
+        tf = flops / (kern_ms * 1e-3) / 1e12
+        out.update(achieved=round(tf, 3), frac=round(tf / FP32_PEAK_TFLOPS, 4),
+                   achieved_basis=("executed FP32 FLOP per frame (rocprofv3 PMC of this build and launch shape) / "
+                                   "live per-frame kernel time" + (", scaled to this rank's triangle tests"
+                                                                  if world > 1 else "")))
+    out["traffic"] = round(traffic) if traffic else None
+    out["valu_issue_utilisation"] = pmc.get("valu_issue_utilisation")
+    out["pmc_source"] = os.path.relpath(args.pmc_json, ROOT)
+    return out
 
 
 def verify_gather(args, full, settings, camera, device, last_frame):
@@ -267,7 +323,7 @@ def verify_gather(args, full, settings, camera, device, last_frame):
         df.next_frame(k, rt.image())
     ref = ref_ctx.read(_lib.IMG_ACCUM)
     ref_ctx.close()
-    got = full.cpu().numpy()
+    got = full if isinstance(full, np.ndarray) else full.cpu().numpy()
     return {"frames": last_frame, "bit_exact": bool(np.array_equal(got, ref)),
             "pixels_differing": int(np.any(got != ref, axis=-1).sum())}
 

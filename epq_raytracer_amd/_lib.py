@@ -13,6 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libhip_raytrace.so")
+DEBUG_LIB_PATH = os.path.join(_HERE, "lib", "libhip_raytrace_debug.so")  # -DHRT_DEBUG_OPTIONS (tests, tools)
 
 # ---- std430 records (assets/raytracing.glsl:51-153) as numpy dtypes + ctypes structs ----------
 
@@ -73,7 +74,10 @@ IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
 OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP, OPT_WQ_NODE_CAP, OPT_PROBE = 5, 6, 7, 8, 9, 10, 11
-OPT_FRAMES_PER_LAUNCH = 12
+OPT_FRAMES_PER_LAUNCH, OPT_OVERLAP = 12, 13
+DEBUG_OPT_FAIL_ALLOC = 1001  # libhip_raytrace_debug.so only
+COMM_ID_BYTES = 128
+COMM_NONE, COMM_RCCL, COMM_RCCL_GROUP, COMM_DEVICE_COPY = 0, 1, 2, 3
 # hrt_kernel (include/hip_raytrace.h)
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
 KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS, KERNEL_BUNDLE_BVH_LDS, KERNEL_BUNDLE_WQ = 6, 7, 8, 9
@@ -100,11 +104,11 @@ SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh
 
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).
 EXPORTED_SYMBOLS = (
-    "hrt_abi_version", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate", "hrt_compute_n",
+    "hrt_abi_version", "hrt_build_id", "hrt_debug_build", "hrt_debug_check_guards", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate", "hrt_compute_n",
     "hrt_read_image", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
     "hrt_get_diagnostics", "hrt_get_tile_profile", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
     "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory",
-    "hrt_stream", "hrt_last_error",
+    "hrt_stream", "hrt_last_error", "hrt_comm_unique_id", "hrt_comm_init", "hrt_comm_init_all", "hrt_comm_info",
     "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
     "hrt_debug_bvh_build", "hrt_debug_bvh_wq_nodes",
     "hrt_obj_load", "hrt_obj_num_meshes", "hrt_obj_mesh", "hrt_obj_free",
@@ -119,15 +123,16 @@ class HrtError(RuntimeError):
         super().__init__(f"{where} failed: {STATUS_NAMES.get(status, status)}{': ' + detail if detail else ''}")
 
 
-_lib = None
+_libs = {}
 
 
-def load() -> ctypes.CDLL:
-    """Load libhip_raytrace.so (raises if it has not been built)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    path = os.environ.get("HRT_LIB", LIB_PATH)  # A/B builds of the same ABI (tools/kbench.py experiments)
+def load(debug: bool = False) -> ctypes.CDLL:
+    """Load libhip_raytrace.so, or with debug=True libhip_raytrace_debug.so (the same objects with the
+    diagnostics-only options compiled in).  Raises if the library has not been built."""
+    if debug in _libs:
+        return _libs[debug]
+    # HRT_LIB: A/B builds of the same ABI (tools/kbench.py experiments)
+    path = DEBUG_LIB_PATH if debug else os.environ.get("HRT_LIB", LIB_PATH)
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                            " or `make -C epq_raytracer_amd/csrc` (no CPU fallback exists)")
@@ -135,6 +140,13 @@ def load() -> ctypes.CDLL:
     P = c_void_p
     sig = {
         "hrt_abi_version": (c_uint32, []),
+        "hrt_debug_build": (c_uint32, []),
+        "hrt_build_id": (c_char_p, []),
+        "hrt_debug_check_guards": (c_int32, [P, POINTER(c_uint32), POINTER(c_uint32)]),
+        "hrt_comm_unique_id": (c_int32, [P]),
+        "hrt_comm_init": (c_int32, [P, P, c_uint32, c_uint32]),
+        "hrt_comm_init_all": (c_int32, [P, c_uint32]),
+        "hrt_comm_info": (c_int32, [P, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
         "hrt_create": (c_int32, [POINTER(CreateInfo), POINTER(c_void_p)]),
         "hrt_destroy": (None, [P]),
         "hrt_set_scene": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32]),
@@ -178,13 +190,18 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    _libs[debug] = lib
     return lib
 
 
-def check(status: int, where: str, ctx=None) -> None:
+def build_id() -> str:
+    """hrt_build_id(): hash of the kernel sources + flags the loaded library was built from."""
+    return load().hrt_build_id().decode()
+
+
+def check(status: int, where: str, ctx=None, lib=None) -> None:
     if status != HRT_OK:
-        detail = load().hrt_last_error(ctx)
+        detail = (lib or load()).hrt_last_error(ctx)
         raise HrtError(status, where, detail.decode() if detail else "")
 
 

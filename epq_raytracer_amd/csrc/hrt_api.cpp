@@ -1,14 +1,18 @@
 // hrt_api.cpp -- the C ABI of libhip_raytrace.so (include/hip_raytrace.h).
 //
-// A context owns everything the reference's RayTracePipeline + DiffusePipeline own on the Vulkan
-// side (src/raytrace_pipeline.rs:31-46, src/diffuse.rs:22-30): the scene buffers, the trace image,
-// the accumulated image, the queue (here: one HIP stream) -- plus the device counters and timing
-// events that the reference does not have.  Memory is allocated once per context; hrt_trace and
-// hrt_accumulate only enqueue kernels (no allocation, no host sync), so a caller may capture them.
+// The context (hrt_context.h) owns everything the reference's RayTracePipeline + DiffusePipeline own
+// on the Vulkan side (src/raytrace_pipeline.rs:31-46, src/diffuse.rs:22-30).  Memory is allocated by
+// hrt_create, hrt_set_scene and hrt_set_option; hrt_trace and hrt_accumulate only enqueue work (no
+// allocation) and block only when kMaxPending timed traces are still outstanding.  hrt_compute_n
+// allocates its frame images on first use.
+//
+// Built twice: libhip_raytrace.so (production) and, with -DHRT_DEBUG_OPTIONS, libhip_raytrace_debug.so,
+// which also accepts the diagnostics-only options (HRT_OPT_PRIORITY = 2, HRT_OPT_GRID_CUS,
+// HRT_DEBUG_OPT_FAIL_ALLOC) that leave frames incomplete or inject failures.
 #include <hip/hip_runtime.h>
 
-#include <cstdio>
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -16,6 +20,7 @@
 
 #include "hip_raytrace.h"
 #include "hrt_bvh.h"
+#include "hrt_context.h"
 #include "hrt_host.h"
 #include "hrt_kernels.h"
 
@@ -31,90 +36,47 @@ static_assert(offsetof(hrt_push_constants, height) == 120, "push layout");
 namespace {
 
 thread_local std::string g_create_error;
-constexpr int kNumCounters = 3 + HRT_NUM_DIAG;  // segments, triangle tests, wave steps, diagnostics
+constexpr size_t kMaxPending = 256;              // timed traces held before the oldest is harvested
+constexpr size_t kStagingChunk = (size_t)8 << 20;  // pinned upload chunk (two of them)
 
-struct EventPair {
-  hipEvent_t start = nullptr, stop = nullptr;
-  uint32_t frames = 1;  // frames the timed launch traced
-};
+template <typename T>
+void free_dev(hrt_context* ctx, T*& p) {
+  hrt::dev_free(ctx, (void*)p);
+  p = nullptr;
+}
+
+// Folds the oldest timed trace into the stats (blocks until it has finished).
+hrt_status harvest_one(hrt_context* ctx) {
+  hrt::EventPair ev = ctx->pending.front();
+  ctx->pending.erase(ctx->pending.begin());
+  ctx->event_pool.push_back(ev);
+  HRT_HIP(ctx, hipEventSynchronize(ev.stop));
+  float ms = 0.0f;
+  HRT_HIP(ctx, hipEventElapsedTime(&ms, ev.start, ev.stop));
+  ctx->last_ms = ms / (float)ev.frames;  // per frame
+  ctx->total_ms += ms;
+  return HRT_OK;
+}
+
+hrt_status harvest_events(hrt_context* ctx) {
+  while (!ctx->pending.empty()) {
+    hrt_status st = harvest_one(ctx);
+    if (st != HRT_OK) return st;
+  }
+  return HRT_OK;
+}
+
+// Every stream of the context drained.
+hrt_status sync_all(hrt_context* ctx) {
+  for (auto& l : ctx->lane)
+    if (l.stream) HRT_HIP(ctx, hipStreamSynchronize(l.stream));
+  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HRT_OK;
+}
 
 }  // namespace
 
-struct hrt_context {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  uint32_t width = 0, height = 0, mode = HRT_MODE_RGBA8;
-  uint32_t row_tile = 0, part_index = 0, part_count = 1, local_rows = 0;
-
-  float4* rays = nullptr;
-  hrt_sphere* spheres = nullptr;
-  hrt_triangle* tris = nullptr;
-  hrt_mesh* meshes = nullptr;
-  uint32_t n_rays = 0, n_spheres = 0, n_tris = 0, n_meshes = 0;
-  bool scene_set = false;
-
-  uint32_t* trace8 = nullptr;
-  uint32_t* accum8 = nullptr;
-  float4* trace32 = nullptr;
-  float4* accum32 = nullptr;
-  void* scratch = nullptr;  // format conversion for hrt_read_image
-  unsigned long long* counters = nullptr;
-  unsigned long long* tile_cycles = nullptr;  // diagnostics: shader clocks per 8x8 tile of the last trace
-  uint32_t* sched = nullptr;      // persistent kernels' scheduler words (hrt_kernels.h)
-  uint32_t* tile_cost = nullptr;  // per 8x8 tile
-  uint32_t* item_buf = nullptr;   // planned work items (tiles x 64: a heavy tile runs as up to 64 items)
-  bool plan_valid = false;        // tile_cost describes the last trace (same size, persistent kernel)
-  uint32_t split_k = 0, split_prio = 1;  // split 0: auto (per kernel, launch_trace)
-  int32_t split_factor = -1;  // auto
-  uint32_t grid_cus = 0;  // HRT_OPT_GRID_CUS (0: every CU)
-  uint32_t coop = 1;      // HRT_OPT_COOP
-  uint32_t wq_node_cap = 0;  // HRT_OPT_WQ_NODE_CAP (0 = auto)
-  uint32_t probe = 1;        // HRT_OPT_PROBE
-  uint32_t frames_per_launch = 64;  // HRT_OPT_FRAMES_PER_LAUNCH (hrt_compute_n)
-  void* frame_stack = nullptr;      // hrt_compute_n: frame_stack_frames trace images
-  uint32_t frame_stack_frames = 0;
-  uint32_t num_cus = 0;
-  uint32_t* cam_meta = nullptr;   // bundle variants: cam_start[n_meshes], cam_count[n_meshes]
-  uint32_t cam_capacity = 0;      // sum of mesh lengths
-  float4* cam_tris = nullptr;     // compacted camera-facing records (64 B each)
-  float4* cam_cull = nullptr;     // bundle-cull records (80 B each)
-  float4* bvh_nodes = nullptr;    // BUNDLE_BVH hierarchy (hrt_bvh.h), built by hrt_set_scene
-  float4* bvh_wq_nodes = nullptr; // its 48 B node image for BUNDLE_WQ (nullptr above 65535 nodes)
-  float4* bvh_prims = nullptr;
-  float4* bvh_irregular = nullptr;
-  uint32_t* bvh_band_off = nullptr;
-  uint32_t* bvh_entries = nullptr;
-  uint32_t* bvh_keybase = nullptr;
-  uint2* bvh_band = nullptr;       // grazing-band entries, 8 B (hrt_bvh.h kBand*)
-  uint32_t bvh_info[HRT_NUM_SCENE_INFO] = {};  // hrt_get_scene_info
-  float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f;
-  uint32_t bvh_leaf = 4;
-  uint32_t bvh_built_leaf = 4;   // leaf size of the hierarchy the last hrt_set_scene built
-  uint32_t bvh_dir_res = 64;     // direction cells per face edge of its band lists
-
-  int variant = 0;
-  bool counters_on = true;
-  bool diag_on = false;
-  uint32_t sec_batch = 0;  // HRT_OPT_SECONDARY_BATCH (0 = auto per kernel, launch_trace)
-  int last_kernel = 0, last_block = 0;  // what the last hrt_trace launched (hrt_stats)
-
-  struct Import {
-    hipExternalMemory_t mem;
-    void* ptr;
-  };
-  std::vector<Import> imports;           // hrt_import_external_memory (released by hrt_destroy)
-  std::vector<EventPair> event_pool;     // reusable
-  std::vector<EventPair> pending;        // recorded, not yet harvested
-  uint64_t traces = 0, accumulates = 0;
-  float last_ms = 0.0f, total_ms = 0.0f;
-
-  std::string err;
-
-  size_t npix() const { return (size_t)local_rows * width; }
-  size_t num_tiles() const { return (size_t)((width + 7) / 8) * ((local_rows + 7) / 8); }
-};
-
-namespace {
+namespace hrt {
 
 hrt_status fail(hrt_context* ctx, hrt_status st, const std::string& msg) {
   if (ctx)
@@ -129,40 +91,145 @@ hrt_status hip_fail(hrt_context* ctx, hipError_t e, const char* what) {
   return fail(ctx, e == hipErrorOutOfMemory ? HRT_ERR_OUT_OF_MEMORY : HRT_ERR_HIP, msg);
 }
 
-#define HRT_HIP(ctx, call)                                      \
-  do {                                                          \
-    hipError_t e_ = (call);                                     \
-    if (e_ != hipSuccess) return hip_fail((ctx), e_, #call);    \
-  } while (0)
-
-// Make the context's device current for the calling thread (contexts may live on any device).
 hrt_status bind(hrt_context* ctx) {
   HRT_HIP(ctx, hipSetDevice(ctx->device));
   return HRT_OK;
 }
 
-template <typename T>
-void free_dev(T*& p) {
-  if (p) (void)hipFree((void*)p);
-  p = nullptr;
-}
-
-hrt_status harvest_events(hrt_context* ctx) {
-  for (auto& ev : ctx->pending) {
-    HRT_HIP(ctx, hipEventSynchronize(ev.stop));
-    float ms = 0.0f;
-    HRT_HIP(ctx, hipEventElapsedTime(&ms, ev.start, ev.stop));
-    ctx->last_ms = ms / (float)ev.frames;  // per frame
-    ctx->total_ms += ms;
-    ctx->event_pool.push_back(ev);
-  }
-  ctx->pending.clear();
+hrt_status wait_lane(hrt_context* ctx, int l) {
+  if (ctx->lane[l].done_set) HRT_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->lane[l].done, 0));
   return HRT_OK;
 }
 
-}  // namespace
+hrt_status join_lanes(hrt_context* ctx) {
+  for (int l = 0; l < kLanes; ++l) {
+    hrt_status st = wait_lane(ctx, l);
+    if (st != HRT_OK) return st;
+  }
+  return HRT_OK;
+}
+
+hrt_status release_lane(hrt_context* ctx, int l) {
+  HRT_HIP(ctx, hipEventRecord(ctx->lane[l].free, ctx->stream));
+  ctx->lane[l].free_set = true;
+  return HRT_OK;
+}
+
+// Device allocations.  The debug build surrounds every allocation with kGuardBytes of a fixed
+// pattern on each side (hrt_debug_check_guards verifies them: a kernel writing past a buffer's end
+// or before its start shows up there).
+#ifdef HRT_DEBUG_OPTIONS
+constexpr size_t kGuardBytes = 4096;
+constexpr int kGuardByte = 0xA5;
+#endif
+
+hipError_t dev_alloc(hrt_context* ctx, void** p, size_t bytes) {
+#ifdef HRT_DEBUG_OPTIONS
+  char* base = nullptr;
+  hipError_t e = hipMalloc((void**)&base, bytes + 2 * kGuardBytes);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return e;
+  }
+  if ((e = hipMemset(base, kGuardByte, kGuardBytes)) != hipSuccess ||
+      (e = hipMemset(base + kGuardBytes + bytes, kGuardByte, kGuardBytes)) != hipSuccess) {
+    (void)hipFree(base);
+    *p = nullptr;
+    return e;
+  }
+  *p = base + kGuardBytes;
+  ctx->guards.push_back({*p, bytes});
+  return hipSuccess;
+#else
+  (void)ctx;
+  return hipMalloc(p, bytes);
+#endif
+}
+
+void dev_free(hrt_context* ctx, void* p) {
+  if (!p) return;
+#ifdef HRT_DEBUG_OPTIONS
+  for (size_t i = 0; i < ctx->guards.size(); ++i)
+    if (ctx->guards[i].ptr == p) {
+      ctx->guards.erase(ctx->guards.begin() + (long)i);
+      (void)hipFree(static_cast<char*>(p) - kGuardBytes);
+      return;
+    }
+#else
+  (void)ctx;
+#endif
+  (void)hipFree(p);
+}
+
+const void* local_image(hrt_context* ctx, uint32_t image_id) {
+  if (image_id == HRT_IMG_ACCUM) return ctx->accum8 ? (const void*)ctx->accum8 : (const void*)ctx->accum32;
+  if (wait_lane(ctx, ctx->cur_lane) != HRT_OK) return nullptr;
+  return ctx->lane[ctx->cur_lane].image();
+}
+
+void free_scene(hrt_context* ctx, SceneBufs& s, bool keep_rays) {
+  if (!keep_rays) free_dev(ctx, s.rays);
+  free_dev(ctx, s.spheres);
+  free_dev(ctx, s.tris);
+  free_dev(ctx, s.meshes);
+  free_dev(ctx, s.bvh_nodes);
+  free_dev(ctx, s.bvh_wq_nodes);
+  free_dev(ctx, s.bvh_prims);
+  free_dev(ctx, s.bvh_irregular);
+  free_dev(ctx, s.bvh_band_off);
+  free_dev(ctx, s.bvh_band);
+  free_dev(ctx, s.bvh_entries);
+  free_dev(ctx, s.bvh_keybase);
+  for (int l = 0; l < kLanes; ++l) {
+    free_dev(ctx, s.cam_meta[l]);
+    free_dev(ctx, s.cam_tris[l]);
+    free_dev(ctx, s.cam_cull[l]);
+  }
+}
+
+}  // namespace hrt
+
+using hrt::fail;
+using hrt::hip_fail;
+using hrt::bind;
 
 extern "C" uint32_t hrt_abi_version(void) { return HRT_ABI_VERSION; }
+
+extern "C" hrt_status hrt_debug_check_guards(hrt_context* ctx, uint32_t* buffers, uint32_t* corrupted) {
+  if (!ctx || !buffers || !corrupted) return HRT_ERR_INVALID_ARGUMENT;
+  *buffers = *corrupted = 0;
+#ifdef HRT_DEBUG_OPTIONS
+  hrt_status st = hrt_synchronize(ctx);
+  if (st != HRT_OK) return st;
+  std::vector<unsigned char> g(hrt::kGuardBytes);
+  for (const auto& r : ctx->guards) {
+    bool bad = false;
+    for (int side = 0; side < 2 && !bad; ++side) {
+      const char* at = side == 0 ? static_cast<const char*>(r.ptr) - hrt::kGuardBytes : static_cast<const char*>(r.ptr) + r.bytes;
+      HRT_HIP(ctx, hipMemcpy(g.data(), at, g.size(), hipMemcpyDeviceToHost));
+      for (unsigned char b : g) bad |= b != hrt::kGuardByte;
+    }
+    ++*buffers;
+    *corrupted += bad ? 1u : 0u;
+  }
+  return HRT_OK;
+#else
+  return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_debug_check_guards: only libhip_raytrace_debug.so guards buffers");
+#endif
+}
+
+#ifndef HRT_BUILD_ID
+#define HRT_BUILD_ID "unknown"
+#endif
+extern "C" const char* hrt_build_id(void) { return HRT_BUILD_ID; }
+
+extern "C" uint32_t hrt_debug_build(void) {
+#ifdef HRT_DEBUG_OPTIONS
+  return 1u;
+#else
+  return 0u;
+#endif
+}
 
 extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_ctx) {
   g_create_error.clear();
@@ -214,36 +281,45 @@ extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_
   if (st != HRT_OK) return bail(st);
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamCreate"));
-  const size_t np = ctx->npix();
-  if (ctx->mode == HRT_MODE_RGBA8) {
-    if ((e = hipMalloc((void**)&ctx->trace8, np * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(trace)"));
-    if ((e = hipMalloc((void**)&ctx->accum8, np * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(accum)"));
-  } else {
-    if ((e = hipMalloc((void**)&ctx->trace32, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(trace)"));
-    if ((e = hipMalloc((void**)&ctx->accum32, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(accum)"));
-  }
-  if ((e = hipMalloc(&ctx->scratch, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(scratch)"));
-  if ((e = hipMalloc((void**)&ctx->counters, kNumCounters * sizeof(unsigned long long))) != hipSuccess)
-    return bail(hip_fail(ctx, e, "hipMalloc(counters)"));
-  {
-    const size_t tiles = ctx->num_tiles();
-    if ((e = hipMalloc((void**)&ctx->sched, 256 * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(sched)"));
-    if ((e = hipMalloc((void**)&ctx->tile_cost, (tiles ? tiles : 1) * 4)) != hipSuccess)
+  if ((e = hrt::ensure_kernel_attributes(ctx->device)) != hipSuccess)
+    return bail(hip_fail(ctx, e, "hipFuncSetAttribute(dynamic LDS)"));
+  const size_t np = ctx->npix(), tiles = std::max<size_t>(ctx->num_tiles(), 1);
+  for (auto& l : ctx->lane) {
+    if ((e = hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking)) != hipSuccess)
+      return bail(hip_fail(ctx, e, "hipStreamCreate(lane)"));
+    if ((e = hipEventCreateWithFlags(&l.done, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&l.free, hipEventDisableTiming)) != hipSuccess)
+      return bail(hip_fail(ctx, e, "hipEventCreate(lane)"));
+    if (ctx->mode == HRT_MODE_RGBA8)
+      e = hrt::dev_alloc(ctx, (void**)&l.trace8, np * 4);
+    else
+      e = hrt::dev_alloc(ctx, (void**)&l.trace32, np * 16);
+    if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(trace)"));
+    if ((e = hrt::dev_alloc(ctx, (void**)&l.sched, 256 * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(sched)"));
+    if ((e = hrt::dev_alloc(ctx, (void**)&l.tile_cost, tiles * 4)) != hipSuccess)
       return bail(hip_fail(ctx, e, "hipMalloc(tile costs)"));
-    if ((e = hipMalloc((void**)&ctx->item_buf, (tiles ? tiles : 1) * 64 * 4)) != hipSuccess)
+    if ((e = hrt::dev_alloc(ctx, (void**)&l.item_buf, tiles * 64 * 4)) != hipSuccess)
       return bail(hip_fail(ctx, e, "hipMalloc(items)"));
   }
+  if (ctx->mode == HRT_MODE_RGBA8)
+    e = hrt::dev_alloc(ctx, (void**)&ctx->accum8, np * 4);
+  else
+    e = hrt::dev_alloc(ctx, (void**)&ctx->accum32, np * 16);
+  if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(accum)"));
+  if ((e = hrt::dev_alloc(ctx, (void**)&ctx->scratch, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(scratch)"));
+  if ((e = hrt::dev_alloc(ctx, (void**)&ctx->counters, hrt::kNumCounters * sizeof(unsigned long long))) != hipSuccess)
+    return bail(hip_fail(ctx, e, "hipMalloc(counters)"));
   {
     int cus = 0;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device)) != hipSuccess)
       return bail(hip_fail(ctx, e, "hipDeviceGetAttribute(CUs)"));
     ctx->num_cus = cus > 0 ? (uint32_t)cus : 1u;
   }
-  if ((e = hipMemsetAsync(ctx->counters, 0, kNumCounters * sizeof(unsigned long long), ctx->stream)) != hipSuccess)
+  if ((e = hipMemsetAsync(ctx->counters, 0, hrt::kNumCounters * sizeof(unsigned long long), ctx->stream)) != hipSuccess)
     return bail(hip_fail(ctx, e, "hipMemset(counters)"));
   // Fresh images read as the cleared state (0,0,0,1) until the first dispatch writes them.
-  if ((e = hrt::launch_clear(ctx->trace8, ctx->trace32, np, ctx->stream)) != hipSuccess)
-    return bail(hip_fail(ctx, e, "clear"));
+  for (auto& l : ctx->lane)
+    if ((e = hrt::launch_clear(l.trace8, l.trace32, np, ctx->stream)) != hipSuccess) return bail(hip_fail(ctx, e, "clear"));
   if ((e = hrt::launch_clear(ctx->accum8, ctx->accum32, np, ctx->stream)) != hipSuccess)
     return bail(hip_fail(ctx, e, "clear"));
   if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
@@ -254,33 +330,32 @@ extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_
 extern "C" void hrt_destroy(hrt_context* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  for (auto& l : ctx->lane)
+    if (l.stream) (void)hipStreamSynchronize(l.stream);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  free_dev(ctx->rays);
-  free_dev(ctx->spheres);
-  free_dev(ctx->tris);
-  free_dev(ctx->meshes);
-  free_dev(ctx->trace8);
-  free_dev(ctx->accum8);
-  free_dev(ctx->trace32);
-  free_dev(ctx->accum32);
-  free_dev(ctx->scratch);
-  free_dev(ctx->counters);
-  free_dev(ctx->tile_cycles);
-  free_dev(ctx->cam_meta);
-  free_dev(ctx->cam_tris);
-  free_dev(ctx->cam_cull);
-  free_dev(ctx->bvh_nodes);
-  free_dev(ctx->bvh_wq_nodes);
-  free_dev(ctx->bvh_prims);
-  free_dev(ctx->bvh_irregular);
-  free_dev(ctx->bvh_band_off);
-  free_dev(ctx->bvh_band);
-  free_dev(ctx->bvh_entries);
-  free_dev(ctx->bvh_keybase);
-  free_dev(ctx->sched);
-  free_dev(ctx->tile_cost);
-  free_dev(ctx->item_buf);
-  free_dev(ctx->frame_stack);
+  hrt::comm_release(ctx);
+  (void)hipSetDevice(ctx->device);
+  hrt::free_scene(ctx, ctx->scene, false);
+  for (auto& l : ctx->lane) {
+    free_dev(ctx, l.trace8);
+    free_dev(ctx, l.trace32);
+    free_dev(ctx, l.sched);
+    free_dev(ctx, l.tile_cost);
+    free_dev(ctx, l.item_buf);
+    if (l.done) (void)hipEventDestroy(l.done);
+    if (l.free) (void)hipEventDestroy(l.free);
+    if (l.stream) (void)hipStreamDestroy(l.stream);
+  }
+  free_dev(ctx, ctx->accum8);
+  free_dev(ctx, ctx->accum32);
+  free_dev(ctx, ctx->scratch);
+  free_dev(ctx, ctx->counters);
+  free_dev(ctx, ctx->tile_cycles);
+  free_dev(ctx, ctx->frame_stack);
+  for (int i = 0; i < 2; ++i) {
+    if (ctx->staging.buf[i]) (void)hipHostFree(ctx->staging.buf[i]);
+    if (ctx->staging.ev[i]) (void)hipEventDestroy(ctx->staging.ev[i]);
+  }
   for (auto& im : ctx->imports) (void)hipDestroyExternalMemory(im.mem);
   for (auto& ev : ctx->event_pool) {
     (void)hipEventDestroy(ev.start);
@@ -296,13 +371,110 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
 
 namespace {
 
-template <typename T>
-hrt_status upload(hrt_context* ctx, T*& dst, const T* src, uint32_t n, const char* what) {
-  free_dev(dst);
-  const size_t bytes = (size_t)(n ? n : 1) * sizeof(T);  // keep a valid pointer for empty lists
-  HRT_HIP(ctx, hipMalloc((void**)&dst, bytes));
-  if (n) HRT_HIP(ctx, hipMemcpyAsync(dst, src, (size_t)n * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
-  (void)what;
+// hrt_set_scene's device allocations (the debug build can fail the n-th one: HRT_DEBUG_OPT_FAIL_ALLOC).
+struct SceneAlloc {
+  hrt_context* ctx;
+  int64_t count = 0;
+  hipError_t operator()(void** p, size_t bytes) {
+    ++count;
+    if (ctx->debug_fail_alloc > 0 && count == ctx->debug_fail_alloc) return hipErrorOutOfMemory;
+    return hrt::dev_alloc(ctx, p, bytes ? bytes : 16);
+  }
+};
+
+// Host -> device copy through the context's pinned staging chunks: the CPU fills one chunk while the
+// DMA engine drains the other (the reference's upload points, src/raytrace_pipeline.rs:302,337,349,
+// 359,371-372, stage through host-visible buffers the same way).
+hrt_status stage_upload(hrt_context* ctx, void* dst, const void* src, size_t bytes) {
+  auto& s = ctx->staging;
+  if (!s.buf[0]) {
+    for (int i = 0; i < 2; ++i) {
+      HRT_HIP(ctx, hipHostMalloc(&s.buf[i], kStagingChunk, hipHostMallocDefault));
+      HRT_HIP(ctx, hipEventCreateWithFlags(&s.ev[i], hipEventDisableTiming));
+      s.used[i] = false;
+    }
+    s.chunk = kStagingChunk;
+  }
+  for (size_t off = 0, k = 0; off < bytes; off += s.chunk, ++k) {
+    const int i = (int)(k & 1);
+    const size_t n = std::min(s.chunk, bytes - off);
+    if (s.used[i]) HRT_HIP(ctx, hipEventSynchronize(s.ev[i]));  // the DMA has left this chunk
+    std::memcpy(s.buf[i], static_cast<const char*>(src) + off, n);
+    HRT_HIP(ctx, hipMemcpyAsync(static_cast<char*>(dst) + off, s.buf[i], n, hipMemcpyHostToDevice, ctx->stream));
+    HRT_HIP(ctx, hipEventRecord(s.ev[i], ctx->stream));
+    s.used[i] = true;
+  }
+  return HRT_OK;
+}
+
+// Allocate dst (>= 16 B, so empty lists keep a valid pointer) and upload bytes of src into it.
+hrt_status alloc_upload(hrt_context* ctx, SceneAlloc& alloc, void** dst, const void* src, size_t bytes,
+                        const char* what) {
+  if (hipError_t e = alloc(dst, bytes); e != hipSuccess) {
+    *dst = nullptr;
+    return hip_fail(ctx, e, (std::string("hrt_set_scene: hipMalloc(") + what + ")").c_str());
+  }
+  return bytes ? stage_upload(ctx, *dst, src, bytes) : HRT_OK;
+}
+
+// Fills s with a complete device copy of the scene (everything but the kept rays).
+hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays, uint32_t n_rays, bool keep_rays,
+                       const hrt_sphere* spheres, uint32_t n_spheres, const hrt_triangle* tris, uint32_t n_tris,
+                       const hrt_mesh* meshes, uint32_t n_meshes) {
+  SceneAlloc alloc{ctx};
+  hrt_status st;
+  if (keep_rays)
+    s.rays = ctx->scene.rays;
+  else if ((st = alloc_upload(ctx, alloc, (void**)&s.rays, rays, (size_t)n_rays * sizeof(float4), "rays")) != HRT_OK)
+    return st;
+  if ((st = alloc_upload(ctx, alloc, (void**)&s.spheres, spheres, (size_t)n_spheres * 64, "spheres")) != HRT_OK ||
+      (st = alloc_upload(ctx, alloc, (void**)&s.tris, tris, (size_t)n_tris * 64, "triangles")) != HRT_OK ||
+      (st = alloc_upload(ctx, alloc, (void**)&s.meshes, meshes, (size_t)n_meshes * 80, "meshes")) != HRT_OK)
+    return st;
+  uint64_t cap = 0;
+  for (uint32_t m = 0; m < n_meshes; ++m) cap += meshes[m].len;
+  if (cap > 0xFFFFFFFFull) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_set_scene: too many mesh triangles");
+  // bundle-variant buffers, one set per trace lane: per-frame compacted camera-facing records
+  for (int l = 0; l < hrt::kLanes; ++l) {
+    hipError_t e;
+    if ((e = alloc((void**)&s.cam_meta[l], (size_t)(n_meshes ? 2 * n_meshes : 2) * 4)) != hipSuccess ||
+        (e = alloc((void**)&s.cam_tris[l], (size_t)(cap ? cap : 1) * 64)) != hipSuccess ||
+        (e = alloc((void**)&s.cam_cull[l], (size_t)(cap ? cap : 1) * 80)) != hipSuccess)
+      return hip_fail(ctx, e, "hrt_set_scene: hipMalloc(camera lists)");
+  }
+  s.cam_capacity = (uint32_t)cap;
+  // bounce-segment hierarchy (BUNDLE_BVH / BUNDLE_WQ)
+  hrt::BvhHost bvh;
+  const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, ctx->bvh_leaf, bvh);
+  if (built) {
+    auto up = [&](auto*& dst, const auto& v, const char* what) -> hrt_status {
+      return alloc_upload(ctx, alloc, (void**)&dst, v.data(), v.size() * sizeof(v[0]), what);
+    };
+    if ((st = up(s.bvh_nodes, bvh.nodes, "bvh nodes")) != HRT_OK) return st;
+    if (bvh.wq_ok && (st = up(s.bvh_wq_nodes, bvh.wq_nodes, "bvh wq nodes")) != HRT_OK) return st;
+    if ((st = up(s.bvh_prims, bvh.prims, "bvh prims")) != HRT_OK ||
+        (st = up(s.bvh_irregular, bvh.irregular, "bvh irregular")) != HRT_OK ||
+        (st = up(s.bvh_band_off, bvh.band_off, "band offsets")) != HRT_OK ||
+        (st = up(s.bvh_band, bvh.band_list, "band lists")) != HRT_OK ||  // 8 B entries
+        (st = up(s.bvh_entries, bvh.entries, "bvh entries")) != HRT_OK ||
+        (st = up(s.bvh_keybase, bvh.key_base, "bvh key bases")) != HRT_OK)
+      return st;
+  }
+  s.bvh_info[HRT_SCENE_BVH_NODES] = bvh.n_nodes;
+  s.bvh_info[HRT_SCENE_BVH_PRIMS] = bvh.n_prims;
+  s.bvh_info[HRT_SCENE_BVH_IRREGULAR] = bvh.n_irregular;
+  s.bvh_info[HRT_SCENE_BVH_NEVER] = bvh.n_never;
+  s.bvh_info[HRT_SCENE_BVH_BUILT] = built ? 1u : 0u;
+  s.bvh_info[HRT_SCENE_BVH_BAND_ENTRIES] = (uint32_t)(bvh.band_list.size() / 2);
+  s.bvh_info[HRT_SCENE_BVH_SAH_MILLI] = (uint32_t)std::min(1e9, bvh.sah_tri_frac * 1000.0 + 0.5);
+  s.bvh_abs_coef = bvh.abs_coef;
+  s.bvh_rel_t = bvh.rel_t;
+  s.bvh_dir_res = bvh.dir_res;
+  s.bvh_built_leaf = std::max(1u, std::min(ctx->bvh_leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
+  s.n_spheres = n_spheres;
+  s.n_tris = n_tris;
+  s.n_meshes = n_meshes;
+  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
   return HRT_OK;
 }
 
@@ -312,7 +484,8 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
                                     uint32_t n_spheres, const hrt_triangle* tris, uint32_t n_tris,
                                     const hrt_mesh* meshes, uint32_t n_meshes) {
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
-  const bool keep_rays = !rays && n_rays == 0 && ctx->rays && ctx->n_rays == (uint64_t)ctx->width * ctx->height;
+  const bool keep_rays =
+      !rays && n_rays == 0 && ctx->scene.rays && ctx->n_rays == (uint64_t)ctx->width * ctx->height;
   if (!keep_rays && ((uint64_t)n_rays != (uint64_t)ctx->width * ctx->height || !rays))
     return fail(ctx, HRT_ERR_INVALID_ARGUMENT,
                 "hrt_set_scene: need width*height rays (or NULL after hrt_generate_rays)");
@@ -325,68 +498,22 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   }
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
-  static_assert(sizeof(float4) == sizeof(hrt_ray), "ray record");
-  if (!keep_rays &&
-      (st = upload(ctx, ctx->rays, reinterpret_cast<const float4*>(rays), n_rays, "rays")) != HRT_OK)
+  if ((st = sync_all(ctx)) != HRT_OK) return st;  // no trace in flight reads the buffers replaced below
+  // The new scene is built completely beside the old one and swapped in only on success, so a failed
+  // call (allocation, upload) leaves the previous scene -- buffers and counts -- intact.
+  hrt::SceneBufs s;
+  st = build_scene(ctx, s, rays, n_rays, keep_rays, spheres, n_spheres, tris, n_tris, meshes, n_meshes);
+  if (st != HRT_OK) {
+    (void)hipStreamSynchronize(ctx->stream);
+    hrt::free_scene(ctx, s, keep_rays);
+    ctx->debug_fail_alloc = 0;
     return st;
-  if ((st = upload(ctx, ctx->spheres, spheres, n_spheres, "spheres")) != HRT_OK) return st;
-  if ((st = upload(ctx, ctx->tris, tris, n_tris, "triangles")) != HRT_OK) return st;
-  if ((st = upload(ctx, ctx->meshes, meshes, n_meshes, "meshes")) != HRT_OK) return st;
-  uint64_t cap = 0;
-  for (uint32_t m = 0; m < n_meshes; ++m) cap += meshes[m].len;
-  if (cap > 0xFFFFFFFFull) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_set_scene: too many mesh triangles");
-  // bundle-variant buffers: per-frame compacted camera-facing records (filled by camera_lists)
-  free_dev(ctx->cam_meta);
-  free_dev(ctx->cam_tris);
-  free_dev(ctx->cam_cull);
-  HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_meta, (size_t)(n_meshes ? 2 * n_meshes : 2) * 4));
-  HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_tris, (size_t)(cap ? cap : 1) * 64));
-  HRT_HIP(ctx, hipMalloc((void**)&ctx->cam_cull, (size_t)(cap ? cap : 1) * 80));
-  ctx->cam_capacity = (uint32_t)cap;
-  // bounce-segment hierarchy (BUNDLE_BVH)
-  hrt::BvhHost bvh;
-  const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, ctx->bvh_leaf, bvh);
-  free_dev(ctx->bvh_nodes);
-  free_dev(ctx->bvh_wq_nodes);
-  free_dev(ctx->bvh_prims);
-  free_dev(ctx->bvh_irregular);
-  free_dev(ctx->bvh_band_off);
-  free_dev(ctx->bvh_band);
-  free_dev(ctx->bvh_entries);
-  free_dev(ctx->bvh_keybase);
-  if (built) {
-    auto up = [&](auto*& dst, const auto& v) -> hrt_status {
-      const size_t bytes = v.size() * sizeof(v[0]);
-      HRT_HIP(ctx, hipMalloc((void**)&dst, bytes ? bytes : 16));
-      if (bytes) HRT_HIP(ctx, hipMemcpyAsync(dst, v.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
-      return HRT_OK;
-    };
-    if ((st = up(ctx->bvh_nodes, bvh.nodes)) != HRT_OK) return st;
-    if (bvh.wq_ok && (st = up(ctx->bvh_wq_nodes, bvh.wq_nodes)) != HRT_OK) return st;
-    if ((st = up(ctx->bvh_prims, bvh.prims)) != HRT_OK) return st;
-    if ((st = up(ctx->bvh_irregular, bvh.irregular)) != HRT_OK) return st;
-    if ((st = up(ctx->bvh_band_off, bvh.band_off)) != HRT_OK) return st;
-    if ((st = up(ctx->bvh_band, bvh.band_list)) != HRT_OK) return st;  // 8 B entries
-    if ((st = up(ctx->bvh_entries, bvh.entries)) != HRT_OK) return st;
-    if ((st = up(ctx->bvh_keybase, bvh.key_base)) != HRT_OK) return st;
   }
-  ctx->bvh_info[0] = bvh.n_nodes;
-  ctx->bvh_info[1] = bvh.n_prims;
-  ctx->bvh_info[2] = bvh.n_irregular;
-  ctx->bvh_info[3] = bvh.n_never;
-  ctx->bvh_info[4] = built ? 1u : 0u;
-  ctx->bvh_abs_coef = bvh.abs_coef;
-  ctx->bvh_dir_res = bvh.dir_res;
-  ctx->bvh_built_leaf = std::max(1u, std::min(ctx->bvh_leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
-  ctx->bvh_rel_t = bvh.rel_t;
-  ctx->bvh_info[5] = (uint32_t)(bvh.band_list.size() / 2);
-  ctx->bvh_info[6] = (uint32_t)std::min(1e9, bvh.sah_tri_frac * 1000.0 + 0.5);
-  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));  // host arrays are only borrowed
+  hrt::free_scene(ctx, ctx->scene, keep_rays);
+  ctx->scene = s;
+  ctx->debug_fail_alloc = 0;
   if (!keep_rays) ctx->n_rays = n_rays;
-  ctx->plan_valid = false;  // tile costs describe the old scene
-  ctx->n_spheres = n_spheres;
-  ctx->n_tris = n_tris;
-  ctx->n_meshes = n_meshes;
+  for (auto& l : ctx->lane) l.plan_valid = false;  // tile costs describe the old scene
   ctx->scene_set = true;
   return HRT_OK;
 }
@@ -398,21 +525,23 @@ hrt_status check_dispatch(hrt_context* ctx, const hrt_push_constants* pc, const 
   if (!ctx->scene_set) return fail(ctx, HRT_ERR_NO_SCENE, std::string(who) + ": hrt_set_scene has not been called");
   if (pc->width != ctx->width || pc->height != ctx->height)
     return fail(ctx, HRT_ERR_INVALID_ARGUMENT, std::string(who) + ": push constant width/height differ from the context");
-  if (pc->num_spheres < 0 || (uint32_t)pc->num_spheres > ctx->n_spheres || pc->num_meshes < 0 ||
-      (uint32_t)pc->num_meshes > ctx->n_meshes)
+  if (pc->num_spheres < 0 || (uint32_t)pc->num_spheres > ctx->scene.n_spheres || pc->num_meshes < 0 ||
+      (uint32_t)pc->num_meshes > ctx->scene.n_meshes)
     return fail(ctx, HRT_ERR_INVALID_ARGUMENT, std::string(who) + ": num_spheres/num_meshes exceed the uploaded scene");
   return HRT_OK;
 }
 
-// The kernel argument block of a dispatch of pc into the context's trace image.
-hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc) {
+// The kernel argument block of a dispatch of pc into trace lane l's image.
+hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int l) {
+  const hrt::SceneBufs& s = ctx->scene;
+  const hrt::Lane& lane = ctx->lane[l];
   hrt::TraceParams p{};
-  p.rays = ctx->rays;
-  p.spheres = ctx->spheres;
-  p.tris = ctx->tris;
-  p.meshes = ctx->meshes;
-  p.img8 = ctx->trace8;
-  p.img32 = ctx->trace32;
+  p.rays = s.rays;
+  p.spheres = s.spheres;
+  p.tris = s.tris;
+  p.meshes = s.meshes;
+  p.img8 = lane.trace8;
+  p.img32 = lane.trace32;
   p.counters = ctx->counters_on ? ctx->counters : nullptr;
   p.diag = ctx->diag_on ? ctx->counters + 3 : nullptr;
   p.tile_cycles = ctx->diag_on ? ctx->tile_cycles : nullptr;
@@ -421,40 +550,41 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc) {
   p.row_tile = ctx->row_tile;
   p.part_index = ctx->part_index;
   p.part_count = ctx->part_count;
-  p.n_tris = ctx->n_tris;
-  p.cam_start = ctx->cam_meta;
-  p.cam_count = ctx->cam_meta + ctx->n_meshes;
-  p.cam_list_capacity = ctx->cam_capacity;
-  p.cam_tris = ctx->cam_tris;
-  p.cam_cull = ctx->cam_cull;
+  p.n_tris = s.n_tris;
+  p.cam_start = s.cam_meta[l];
+  p.cam_count = s.cam_meta[l] + s.n_meshes;
+  p.cam_list_capacity = s.cam_capacity;
+  p.cam_tris = s.cam_tris[l];
+  p.cam_cull = s.cam_cull[l];
   p.sec_batch = ctx->sec_batch;
-  p.sched = ctx->sched;
-  p.tile_cost = ctx->tile_cost;
-  p.item_buf = ctx->item_buf;
+  p.sched = lane.sched;
+  p.tile_cost = lane.tile_cost;
+  p.item_buf = lane.item_buf;
   p.split_k = ctx->split_k;
   p.split_factor = ctx->split_factor;
   p.split_prio = ctx->split_prio;
   p.coop = ctx->coop;
   p.wq_ncap = ctx->wq_node_cap;  // request; launch_trace sizes the stacks
-  p.plan_valid = ctx->plan_valid ? 1u : 0u;
+  p.plan_valid = lane.plan_valid ? 1u : 0u;
   p.num_cus = ctx->grid_cus ? std::min(ctx->grid_cus, ctx->num_cus) : ctx->num_cus;
-  p.bvh_nodes = ctx->bvh_info[4] ? ctx->bvh_nodes : nullptr;
-  p.bvh_wq_nodes = ctx->bvh_info[4] ? ctx->bvh_wq_nodes : nullptr;
-  p.bvh_prims = ctx->bvh_prims;
-  p.bvh_irregular = ctx->bvh_irregular;
-  p.bvh_band_off = ctx->bvh_band_off;
-  p.bvh_dir_res = ctx->bvh_dir_res;
-  p.bvh_sah_milli = ctx->bvh_info[6];
-  p.bvh_band = ctx->bvh_band;
-  p.bvh_entries = ctx->bvh_entries;
-  p.bvh_keybase = ctx->bvh_keybase;
-  p.bvh_n_prims = ctx->bvh_info[1];
-  p.bvh_n_meshes = ctx->n_meshes;
-  p.bvh_n_nodes = ctx->bvh_info[0];
-  p.bvh_abs_coef = ctx->bvh_abs_coef;
-  p.bvh_rel_t = ctx->bvh_rel_t;
-  p.bvh_n_irregular = ctx->bvh_info[2];
-  p.bvh_max_leaf = ctx->bvh_built_leaf;
+  const bool built = s.bvh_info[HRT_SCENE_BVH_BUILT] != 0;
+  p.bvh_nodes = built ? s.bvh_nodes : nullptr;
+  p.bvh_wq_nodes = built ? s.bvh_wq_nodes : nullptr;
+  p.bvh_prims = s.bvh_prims;
+  p.bvh_irregular = s.bvh_irregular;
+  p.bvh_band_off = s.bvh_band_off;
+  p.bvh_dir_res = s.bvh_dir_res;
+  p.bvh_sah_milli = s.bvh_info[HRT_SCENE_BVH_SAH_MILLI];
+  p.bvh_band = s.bvh_band;
+  p.bvh_entries = s.bvh_entries;
+  p.bvh_keybase = s.bvh_keybase;
+  p.bvh_n_prims = s.bvh_info[HRT_SCENE_BVH_PRIMS];
+  p.bvh_n_meshes = s.n_meshes;
+  p.bvh_n_nodes = s.bvh_info[HRT_SCENE_BVH_NODES];
+  p.bvh_abs_coef = s.bvh_abs_coef;
+  p.bvh_rel_t = s.bvh_rel_t;
+  p.bvh_n_irregular = s.bvh_info[HRT_SCENE_BVH_IRREGULAR];
+  p.bvh_max_leaf = s.bvh_built_leaf;
   p.n_frames = 1;
   p.frame_stride = ctx->npix();
   return p;
@@ -464,16 +594,17 @@ bool persistent_kernel(int k) {
   return k == HRT_KERNEL_BUNDLE_WQ || k == HRT_KERNEL_BUNDLE_CULL_LDS || k == HRT_KERNEL_BUNDLE_BVH_LDS;
 }
 
-// One trace launch of p.n_frames frames (timed by a HIP event pair counted as that many traces).
-hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p) {
-  if (ctx->diag_on && !ctx->tile_cycles) {
-    HRT_HIP(ctx, hipMalloc((void**)&ctx->tile_cycles, ctx->num_tiles() * 4 * sizeof(unsigned long long)));
-    p.tile_cycles = ctx->tile_cycles;
-  }
+// One trace launch of p.n_frames frames on `stream` with lane l's planner buffers (timed by a HIP
+// event pair counted as that many traces).
+hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stream, int l) {
   if (ctx->diag_on)
-    HRT_HIP(ctx, hipMemsetAsync(ctx->tile_cycles, 0, ctx->num_tiles() * 4 * sizeof(unsigned long long), ctx->stream));
+    HRT_HIP(ctx, hipMemsetAsync(ctx->tile_cycles, 0, ctx->num_tiles() * 4 * sizeof(unsigned long long), stream));
   const int variant = ctx->variant;
-  EventPair ev;
+  if (ctx->pending.size() >= kMaxPending) {
+    hrt_status st = harvest_one(ctx);
+    if (st != HRT_OK) return st;
+  }
+  hrt::EventPair ev;
   if (!ctx->event_pool.empty()) {
     ev = ctx->event_pool.back();
     ctx->event_pool.pop_back();
@@ -482,38 +613,56 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p) {
     HRT_HIP(ctx, hipEventCreate(&ev.stop));
   }
   ev.frames = p.n_frames > 1 ? p.n_frames : 1u;
-  // First trace of a persistent kernel (no tile costs yet): a 1-sample probe trace into the scratch
-  // image measures the tiles' relative costs so that this trace already follows a plan (HRT_OPT_PROBE).
+  hrt::Lane& lane = ctx->lane[l];
+  // First trace of a persistent kernel on this lane (no tile costs yet): a 1-sample probe trace into the
+  // lane's own image (fully overwritten by the trace that follows on the same stream) measures the
+  // tiles' relative costs so that this trace already follows a plan (HRT_OPT_PROBE).
   const int resolved = hrt::resolve_variant(p, variant);
-  if (ctx->probe && !ctx->plan_valid && ctx->num_tiles() >= 1024 && persistent_kernel(resolved)) {
+  if (ctx->probe && !lane.plan_valid && ctx->num_tiles() >= 1024 && persistent_kernel(resolved)) {
     hrt::TraceParams q = p;
     q.pc.num_samples = 1;
     q.n_frames = 1;
-    q.img8 = ctx->trace8 ? reinterpret_cast<uint32_t*>(ctx->scratch) : nullptr;
-    q.img32 = ctx->trace32 ? reinterpret_cast<float4*>(ctx->scratch) : nullptr;
+    q.img8 = lane.trace8;
+    q.img32 = lane.trace32;
     q.counters = nullptr;
     q.diag = nullptr;
     q.tile_cycles = nullptr;
     q.probe = 1u;
     int ran = 0, blk = 0;
-    if (hipError_t pe = hrt::launch_trace(q, variant, ctx->stream, &ran, &blk); pe != hipSuccess) {
+    if (hipError_t pe = hrt::launch_trace(q, variant, stream, &ran, &blk); pe != hipSuccess) {
       ctx->event_pool.push_back(ev);
       return hip_fail(ctx, pe, "probe trace launch");
     }
     p.plan_valid = 1u;
   }
-  HRT_HIP(ctx, hipEventRecord(ev.start, ctx->stream));
-  hipError_t e = hrt::launch_trace(p, variant, ctx->stream, &ctx->last_kernel, &ctx->last_block);
-  // the persistent kernels recorded this trace's tile costs: the next one can follow a plan
-  ctx->plan_valid = e == hipSuccess && persistent_kernel(ctx->last_kernel);
+  HRT_HIP(ctx, hipEventRecord(ev.start, stream));
+  hipError_t e = hrt::launch_trace(p, variant, stream, &ctx->last_kernel, &ctx->last_block);
+  // the persistent kernels recorded this trace's tile costs: the lane's next trace can follow a plan
+  lane.plan_valid = e == hipSuccess && persistent_kernel(ctx->last_kernel);
   if (e != hipSuccess) {
     ctx->event_pool.push_back(ev);
     return hip_fail(ctx, e, "trace kernel launch");
   }
-  HRT_HIP(ctx, hipEventRecord(ev.stop, ctx->stream));
+  HRT_HIP(ctx, hipEventRecord(ev.stop, stream));
   ctx->pending.push_back(ev);
   ctx->traces += ev.frames;
-  if (ctx->pending.size() > 256) return harvest_events(ctx);  // bound the pending list
+  return HRT_OK;
+}
+
+// The lane the next trace runs on (alternating with HRT_OPT_OVERLAP, after the lane's last reader).
+hrt_status begin_lane(hrt_context* ctx, int* out) {
+  const int l = ctx->overlap && !ctx->diag_on && ctx->lane_used ? ctx->cur_lane ^ 1 : 0;
+  hrt::Lane& lane = ctx->lane[l];
+  if (lane.free_set) HRT_HIP(ctx, hipStreamWaitEvent(lane.stream, lane.free, 0));
+  *out = l;
+  return HRT_OK;
+}
+
+hrt_status end_lane(hrt_context* ctx, int l) {
+  HRT_HIP(ctx, hipEventRecord(ctx->lane[l].done, ctx->lane[l].stream));
+  ctx->lane[l].done_set = true;
+  ctx->cur_lane = l;
+  ctx->lane_used = true;
   return HRT_OK;
 }
 
@@ -523,13 +672,17 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   if (!ctx || !pc) return HRT_ERR_INVALID_ARGUMENT;
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
+  if (!pc->init && (st = check_dispatch(ctx, pc, "hrt_trace")) != HRT_OK) return st;
+  int l = 0;
+  if ((st = begin_lane(ctx, &l)) != HRT_OK) return st;
+  hrt::Lane& lane = ctx->lane[l];
   if (pc->init) {  // RayTracePipeline::init, src/raytrace_pipeline.rs:190-213
-    HRT_HIP(ctx, hrt::launch_clear(ctx->trace8, ctx->trace32, ctx->npix(), ctx->stream));
-    return HRT_OK;
+    HRT_HIP(ctx, hrt::launch_clear(lane.trace8, lane.trace32, ctx->npix(), lane.stream));
+  } else {
+    hrt::TraceParams p = make_params(ctx, pc, l);
+    if ((st = launch_frames(ctx, p, lane.stream, l)) != HRT_OK) return st;
   }
-  if ((st = check_dispatch(ctx, pc, "hrt_trace")) != HRT_OK) return st;
-  hrt::TraceParams p = make_params(ctx, pc);
-  return launch_frames(ctx, p);
+  return end_lane(ctx, l);
 }
 
 extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* pc, uint32_t n) {
@@ -538,16 +691,21 @@ extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* 
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
   if ((st = check_dispatch(ctx, pc, "hrt_compute_n")) != HRT_OK) return st;
-  hrt::TraceParams p = make_params(ctx, pc);
-  const size_t np = ctx->npix(), px_bytes = ctx->trace8 ? 4 : 16;
+  if (n == 0) return HRT_OK;
+  // The whole loop runs on the context stream with lane 0's buffers, after every lane's last trace.
+  if ((st = hrt::join_lanes(ctx)) != HRT_OK) return st;
+  hrt::TraceParams p = make_params(ctx, pc, 0);
+  hrt::Lane& lane = ctx->lane[0];
+  const size_t np = ctx->npix(), px_bytes = ctx->px_bytes();
   // Frames per launch: up to HRT_OPT_FRAMES_PER_LAUNCH, and at most 1 GiB of frame images.
   const uint32_t cap = (uint32_t)std::max<size_t>(
       1, std::min<size_t>(ctx->frames_per_launch, ((size_t)1 << 30) / std::max<size_t>(np * px_bytes, 1)));
   const bool batch = persistent_kernel(hrt::resolve_variant(p, ctx->variant)) && cap > 1 && n > 1;
   if (batch && ctx->frame_stack_frames < std::min(cap, n)) {
-    free_dev(ctx->frame_stack);
+    HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    free_dev(ctx, ctx->frame_stack);
     ctx->frame_stack_frames = 0;
-    HRT_HIP(ctx, hipMalloc(&ctx->frame_stack, (size_t)std::min(cap, n) * np * px_bytes));
+    HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->frame_stack, (size_t)std::min(cap, n) * np * px_bytes));
     ctx->frame_stack_frames = std::min(cap, n);
   }
   for (uint32_t done = 0; done < n;) {
@@ -557,71 +715,85 @@ extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* 
     hrt::TraceParams q = p;
     q.pc.rng_offset = pc->rng_offset + done;  // u32, wrapping like the per-frame loop's pushes
     q.n_frames = nf;
-    q.plan_valid = ctx->plan_valid ? 1u : 0u;
+    q.plan_valid = lane.plan_valid ? 1u : 0u;
     if (nf > 1) {
-      q.img8 = ctx->trace8 ? reinterpret_cast<uint32_t*>(ctx->frame_stack) : nullptr;
-      q.img32 = ctx->trace32 ? reinterpret_cast<float4*>(ctx->frame_stack) : nullptr;
+      q.img8 = lane.trace8 ? reinterpret_cast<uint32_t*>(ctx->frame_stack) : nullptr;
+      q.img32 = lane.trace32 ? reinterpret_cast<float4*>(ctx->frame_stack) : nullptr;
     }
-    if ((st = launch_frames(ctx, q)) != HRT_OK) return st;
+    if ((st = launch_frames(ctx, q, ctx->stream, 0)) != HRT_OK) return st;
     for (uint32_t f = 0; f < nf; ++f) {  // DiffusePipeline::next_frame(frame) in frame order
-      const uint32_t* t8 = nf > 1 && q.img8 ? q.img8 + f * np : ctx->trace8;
-      const float4* t32 = nf > 1 && q.img32 ? q.img32 + f * np : ctx->trace32;
+      const uint32_t* t8 = nf > 1 && q.img8 ? q.img8 + f * np : lane.trace8;
+      const float4* t32 = nf > 1 && q.img32 ? q.img32 + f * np : lane.trace32;
       HRT_HIP(ctx, hrt::launch_accumulate(ctx->accum8, t8, ctx->accum32, t32, np, q.pc.rng_offset + f, ctx->stream));
       ctx->accumulates++;
     }
     if (nf > 1)  // the trace image holds the last frame, as after the per-frame loop
-      HRT_HIP(ctx, hipMemcpyAsync(ctx->trace8 ? (void*)ctx->trace8 : (void*)ctx->trace32,
-                                  static_cast<const char*>(ctx->frame_stack) + (size_t)(nf - 1) * np * px_bytes,
+      HRT_HIP(ctx, hipMemcpyAsync(lane.image(), static_cast<const char*>(ctx->frame_stack) + (size_t)(nf - 1) * np * px_bytes,
                                   np * px_bytes, hipMemcpyDeviceToDevice, ctx->stream));
     done += nf;
   }
-  return HRT_OK;
+  ctx->cur_lane = 0;
+  ctx->lane_used = true;
+  return hrt::release_lane(ctx, 0);  // lane 0's next trace follows this loop
 }
 
 extern "C" hrt_status hrt_accumulate(hrt_context* ctx, uint32_t frame) {
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
-  HRT_HIP(ctx, hrt::launch_accumulate(ctx->accum8, ctx->trace8, ctx->accum32, ctx->trace32, ctx->npix(), frame,
+  const int l = ctx->cur_lane;  // next_image = the most recent trace
+  if ((st = hrt::wait_lane(ctx, l)) != HRT_OK) return st;
+  const hrt::Lane& lane = ctx->lane[l];
+  HRT_HIP(ctx, hrt::launch_accumulate(ctx->accum8, lane.trace8, ctx->accum32, lane.trace32, ctx->npix(), frame,
                                       ctx->stream));
   ctx->accumulates++;
-  return HRT_OK;
+  return hrt::release_lane(ctx, l);
 }
 
-extern "C" hrt_status hrt_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes) {
-  if (!ctx || !dst) return HRT_ERR_INVALID_ARGUMENT;
-  if (image_id != HRT_IMG_TRACE && image_id != HRT_IMG_ACCUM)
-    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown image id");
-  if (fmt != HRT_FMT_RGBA8 && fmt != HRT_FMT_RGBA32F)
-    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown format");
-  const size_t np = ctx->npix();
-  const size_t need = np * (fmt == HRT_FMT_RGBA8 ? 4 : 16);
-  if (bytes < need) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: destination too small");
-  hrt_status st = bind(ctx);
-  if (st != HRT_OK) return st;
-  const bool accum = image_id == HRT_IMG_ACCUM;
-  const void* src = nullptr;
-  if (ctx->mode == HRT_MODE_RGBA8) {
-    const uint32_t* s8 = accum ? ctx->accum8 : ctx->trace8;
-    if (fmt == HRT_FMT_RGBA8) {
-      src = s8;
-    } else {
-      HRT_HIP(ctx, hrt::launch_convert(s8, (float4*)ctx->scratch, nullptr, nullptr, np, ctx->stream));
-      src = ctx->scratch;
-    }
-  } else {
-    const float4* s32 = accum ? ctx->accum32 : ctx->trace32;
-    if (fmt == HRT_FMT_RGBA32F) {
-      src = s32;
-    } else {
-      HRT_HIP(ctx, hrt::launch_convert(nullptr, nullptr, s32, (uint32_t*)ctx->scratch, np, ctx->stream));
-      src = ctx->scratch;
-    }
+namespace {
+
+// dst <- src (npix pixels of the context's format) in format fmt, ordered on ctx->stream; blocking.
+hrt_status copy_out(hrt_context* ctx, const void* src, size_t npix, uint32_t fmt, void* dst, void* scratch) {
+  const size_t need = npix * (fmt == HRT_FMT_RGBA8 ? 4 : 16);
+  const bool native = (ctx->mode == HRT_MODE_RGBA8) == (fmt == HRT_FMT_RGBA8);
+  if (!native) {
+    if (ctx->mode == HRT_MODE_RGBA8)
+      HRT_HIP(ctx, hrt::launch_convert((const uint32_t*)src, (float4*)scratch, nullptr, nullptr, npix, ctx->stream));
+    else
+      HRT_HIP(ctx, hrt::launch_convert(nullptr, nullptr, (const float4*)src, (uint32_t*)scratch, npix, ctx->stream));
+    src = scratch;
   }
   HRT_HIP(ctx, hipMemcpyAsync(dst, src, need, hipMemcpyDefault, ctx->stream));
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return HRT_OK;
 }
+
+}  // namespace
+
+extern "C" hrt_status hrt_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes) {
+  if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
+  if (image_id != HRT_IMG_TRACE && image_id != HRT_IMG_ACCUM)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown image id");
+  if (fmt != HRT_FMT_RGBA8 && fmt != HRT_FMT_RGBA32F)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown format");
+  if (ctx->comm) return hrt::comm_read_image(ctx, image_id, fmt, dst, bytes);  // the framebuffer gather
+  if (!dst) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: null destination");
+  const size_t np = ctx->npix();
+  if (bytes < np * (fmt == HRT_FMT_RGBA8 ? 4 : 16))
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: destination too small");
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  const void* src = hrt::local_image(ctx, image_id);
+  if (!src) return fail(ctx, HRT_ERR_HIP, "hrt_read_image: lane wait failed");
+  if ((st = copy_out(ctx, src, np, fmt, dst, ctx->scratch)) != HRT_OK) return st;
+  return image_id == HRT_IMG_TRACE ? hrt::release_lane(ctx, ctx->cur_lane) : HRT_OK;
+}
+
+namespace hrt {
+hrt_status copy_frame_out(hrt_context* ctx, const void* src, size_t npix, uint32_t fmt, void* dst, void* scratch) {
+  return copy_out(ctx, src, npix, fmt, dst, scratch);
+}
+}  // namespace hrt
 
 extern "C" hrt_status hrt_get_layout(const hrt_context* ctx, hrt_layout* out) {
   if (!ctx || !out) return HRT_ERR_INVALID_ARGUMENT;
@@ -639,8 +811,7 @@ extern "C" hrt_status hrt_synchronize(hrt_context* ctx) {
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
-  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  return HRT_OK;
+  return sync_all(ctx);
 }
 
 extern "C" hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out) {
@@ -648,7 +819,7 @@ extern "C" hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out) {
   hrt_status st = hrt_synchronize(ctx);
   if (st != HRT_OK) return st;
   if ((st = harvest_events(ctx)) != HRT_OK) return st;
-  unsigned long long c[kNumCounters] = {};
+  unsigned long long c[hrt::kNumCounters] = {};
   HRT_HIP(ctx, hipMemcpy(c, ctx->counters, sizeof c, hipMemcpyDeviceToHost));
   out->segments = c[0];
   out->tri_tests = c[1];
@@ -666,7 +837,7 @@ extern "C" hrt_status hrt_get_diagnostics(hrt_context* ctx, uint64_t* out, uint3
   if (!ctx || !out || count > HRT_NUM_DIAG) return HRT_ERR_INVALID_ARGUMENT;
   hrt_status st = hrt_synchronize(ctx);
   if (st != HRT_OK) return st;
-  unsigned long long c[kNumCounters] = {};
+  unsigned long long c[hrt::kNumCounters] = {};
   HRT_HIP(ctx, hipMemcpy(c, ctx->counters, sizeof c, hipMemcpyDeviceToHost));
   for (uint32_t i = 0; i < count; ++i) out[i] = c[3 + i];
   return HRT_OK;
@@ -677,15 +848,17 @@ extern "C" hrt_status hrt_generate_rays(hrt_context* ctx, float camera_focal_len
   if (!ctx || !up) return HRT_ERR_INVALID_ARGUMENT;
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
+  if ((st = sync_all(ctx)) != HRT_OK) return st;  // no trace in flight reads the rays
   float first[3], px[3], py[3];
   const uint32_t n = hrt_host_ray_grid(ctx->width, ctx->height, camera_focal_length, viewport_height, up, first, px,
                                        py, default_jitter);
   const size_t want = (size_t)ctx->width * ctx->height;
-  if (!ctx->rays || ctx->n_rays != want) {
-    free_dev(ctx->rays);
-    HRT_HIP(ctx, hipMalloc((void**)&ctx->rays, (want ? want : 1) * sizeof(float4)));
+  if (!ctx->scene.rays || ctx->n_rays != want) {
+    free_dev(ctx, ctx->scene.rays);
+    ctx->n_rays = 0;
+    HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->scene.rays, (want ? want : 1) * sizeof(float4)));
   }
-  if (n) HRT_HIP(ctx, hrt::launch_make_rays(ctx->rays, ctx->width, ctx->height, first, px, py, ctx->stream));
+  if (n) HRT_HIP(ctx, hrt::launch_make_rays(ctx->scene.rays, ctx->width, ctx->height, first, px, py, ctx->stream));
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->n_rays = (uint32_t)want;
   return HRT_OK;
@@ -771,11 +944,11 @@ extern "C" hrt_status hrt_debug_unmap_memory(void* ptr, uint64_t size) {
 }
 
 extern "C" hrt_status hrt_read_rays(hrt_context* ctx, hrt_ray* out, uint32_t n) {
-  if (!ctx || (!out && n) || (uint64_t)n > ctx->n_rays || !ctx->rays)
+  if (!ctx || (!out && n) || (uint64_t)n > ctx->n_rays || !ctx->scene.rays)
     return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_rays: no rays or n too large");
   hrt_status st = hrt_synchronize(ctx);
   if (st != HRT_OK) return st;
-  if (n) HRT_HIP(ctx, hipMemcpy(out, ctx->rays, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
+  if (n) HRT_HIP(ctx, hipMemcpy(out, ctx->scene.rays, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
   return HRT_OK;
 }
 
@@ -790,7 +963,7 @@ extern "C" hrt_status hrt_get_tile_profile(hrt_context* ctx, uint64_t* out, uint
 
 extern "C" hrt_status hrt_get_scene_info(hrt_context* ctx, uint32_t* out, uint32_t count) {
   if (!ctx || !out || count > HRT_NUM_SCENE_INFO) return HRT_ERR_INVALID_ARGUMENT;
-  for (uint32_t i = 0; i < count; ++i) out[i] = ctx->bvh_info[i];
+  for (uint32_t i = 0; i < count; ++i) out[i] = ctx->scene.bvh_info[i];
   return HRT_OK;
 }
 
@@ -799,7 +972,7 @@ extern "C" hrt_status hrt_reset_stats(hrt_context* ctx) {
   hrt_status st = hrt_synchronize(ctx);
   if (st != HRT_OK) return st;
   if ((st = harvest_events(ctx)) != HRT_OK) return st;
-  HRT_HIP(ctx, hipMemsetAsync(ctx->counters, 0, kNumCounters * sizeof(unsigned long long), ctx->stream));
+  HRT_HIP(ctx, hipMemsetAsync(ctx->counters, 0, hrt::kNumCounters * sizeof(unsigned long long), ctx->stream));
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->traces = ctx->accumulates = 0;
   ctx->last_ms = ctx->total_ms = 0.0f;
@@ -816,6 +989,12 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       return HRT_OK;
     case HRT_OPT_COUNTERS:
       if (value < 0 || value > 2) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "counters option must be 0, 1 or 2");
+      if (value == 2 && !ctx->tile_cycles) {  // allocated here, so that hrt_trace never allocates
+        hrt_status st = hrt_synchronize(ctx);
+        if (st != HRT_OK) return st;
+        HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->tile_cycles,
+                               std::max<size_t>(ctx->num_tiles(), 1) * 4 * sizeof(unsigned long long)));
+      }
       ctx->counters_on = value != 0;
       ctx->diag_on = value == 2;
       return HRT_OK;
@@ -835,7 +1014,13 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       ctx->split_factor = (int32_t)value;
       return HRT_OK;
     case HRT_OPT_PRIORITY:
+#ifdef HRT_DEBUG_OPTIONS
       if (value < 0 || value > 2) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "priority must be 0, 1 or 2");
+#else
+      if (value < 0 || value > 1)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT,
+                    "priority must be 0 or 1 (2, heavy tiles only, is in libhip_raytrace_debug.so)");
+#endif
       ctx->split_prio = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_PROBE:
@@ -847,6 +1032,10 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
         return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "frames per launch must be in [1, 1024]");
       ctx->frames_per_launch = (uint32_t)value;
       return HRT_OK;
+    case HRT_OPT_OVERLAP:
+      if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "overlap must be 0 or 1");
+      ctx->overlap = (uint32_t)value;
+      return HRT_OK;
     case HRT_OPT_WQ_NODE_CAP:
       if (value != 0 && (value < 128 || value > (1 << 20)))
         return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "wq node cap must be 0 (auto) or in [128, 2^20]");
@@ -856,15 +1045,25 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "coop must be 0 or 1");
       ctx->coop = (uint32_t)value;
       return HRT_OK;
-    case HRT_OPT_GRID_CUS:
-      if (value < 0) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "grid CUs must be >= 0");
-      ctx->grid_cus = (uint32_t)value;
-      return HRT_OK;
     case HRT_OPT_BVH_LEAF_SIZE:
       if (value < 1 || value > hrt::kBvhMaxLeafCount)
         return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "BVH leaf size must be in [1, 16]");
       ctx->bvh_leaf = (uint32_t)value;
       return HRT_OK;
+#ifdef HRT_DEBUG_OPTIONS
+    case HRT_OPT_GRID_CUS:
+      if (value < 0) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "grid CUs must be >= 0");
+      ctx->grid_cus = (uint32_t)value;
+      return HRT_OK;
+    case HRT_DEBUG_OPT_FAIL_ALLOC:
+      if (value < 0) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "fail-alloc index must be >= 0");
+      ctx->debug_fail_alloc = value;
+      return HRT_OK;
+#else
+    case HRT_OPT_GRID_CUS:
+    case HRT_DEBUG_OPT_FAIL_ALLOC:
+      return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "debug option: only libhip_raytrace_debug.so accepts it");
+#endif
     default:
       return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "unknown option key");
   }

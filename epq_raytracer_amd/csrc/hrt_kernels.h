@@ -68,6 +68,8 @@ struct TraceParams {
   size_t frame_stride;
 };
 
+// Per device, once: the dynamic-LDS limits of the persistent kernels (hipFuncSetAttribute).
+hipError_t ensure_kernel_attributes(int device);
 // Launches the trace kernel(s); *ran / *block receive the resolved hrt_kernel and workgroup size.
 hipError_t launch_trace(const TraceParams& p, int variant, hipStream_t stream, int* ran, int* block);
 int resolve_variant(const TraceParams& p, int variant);  // the kernel an HRT_KERNEL_* request runs
@@ -77,6 +79,10 @@ hipError_t launch_make_rays(float4* rays, uint32_t width, uint32_t height, const
 hipError_t launch_clear(uint32_t* img8, float4* img32, size_t npix, hipStream_t stream);
 hipError_t launch_accumulate(uint32_t* cur8, const uint32_t* new8, float4* cur32, const float4* new32, size_t npix,
                              uint32_t frame, hipStream_t stream);
+// Row-tile framebuffer assembly: gathered = parts x local_rows rows (rank-major), frame = height rows of
+// row_words 4-byte words; global row y comes from part (y / row_tile) % parts (hip_raytrace.h partition).
+hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint32_t row_words, uint32_t height,
+                                uint32_t local_rows, uint32_t row_tile, uint32_t parts, hipStream_t stream);
 hipError_t launch_convert(const uint32_t* src8, float4* dst32, const float4* src32, uint32_t* dst8, size_t npix,
                           hipStream_t stream);
 

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include "hip_raytrace.h"
 #include "hrt_bvh.h"
@@ -2185,6 +2187,21 @@ __global__ __launch_bounds__(256) void f32_to_rgba8(const float4* src, uint32_t*
   dst[i] = unorm8(v.x) | (unorm8(v.y) << 8) | (unorm8(v.z) << 16) | (unorm8(v.w) << 24);
 }
 
+// Row-tile framebuffer assembly after the gather: global row y lives in part
+// (y / row_tile) % parts at local row (y / row_tile / parts) * row_tile + y % row_tile.  One 4-byte word
+// per lane; grid.y = rows, so the row arithmetic is wave-uniform and both sides stream coalesced.
+__global__ __launch_bounds__(256) void assemble_rows(const uint32_t* __restrict__ gathered, uint32_t* __restrict__ frame,
+                                                     uint32_t row_words, uint32_t local_rows, uint32_t row_tile,
+                                                     uint32_t parts) {
+  const uint32_t y = blockIdx.y;
+  const uint32_t t = y / row_tile;
+  const uint32_t part = t % parts;
+  const uint32_t lr = (t / parts) * row_tile + y % row_tile;
+  const uint32_t* src = gathered + ((size_t)part * local_rows + lr) * row_words;
+  uint32_t* dst = frame + (size_t)y * row_words;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < row_words; i += gridDim.x * 256) dst[i] = src[i];
+}
+
 }  // namespace hrt
 
 // ---- launch wrappers (host) ----------------------------------------------------------------------
@@ -2277,27 +2294,41 @@ static hipError_t prepare_schedule(TraceParams& q, hipStream_t stream) {
   return hipMemsetAsync(q.sched, 0, 4, stream);
 }
 
+// The persistent kernels' dynamic-LDS limits, set once per device (hrt_create calls this for its device;
+// the attribute is per device, so every device a context lives on gets its own call).
+hipError_t ensure_kernel_attributes(int device) {
+  static std::mutex mu;
+  static std::vector<char> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (device < 0) return hipErrorInvalidDevice;
+  if ((size_t)device < done.size() && done[(size_t)device]) return hipSuccess;
+  const void* brute[] = {reinterpret_cast<const void*>(&trace_brute_lds)};
+  const void* half_cu[] = {reinterpret_cast<const void*>(&trace_bundle_cull_lds<512, false>),
+                           reinterpret_cast<const void*>(&trace_bundle_cull_lds<512, true>)};
+  const void* whole_cu[] = {reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024, false>),
+                            reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024, true>),
+                            reinterpret_cast<const void*>(&trace_bundle_bvh_lds<false>),
+                            reinterpret_cast<const void*>(&trace_bundle_bvh_lds<true>),
+                            reinterpret_cast<const void*>(&trace_bundle_wq<false>),
+                            reinterpret_cast<const void*>(&trace_bundle_wq<true>)};
+  hipError_t e;
+  for (const void* f : brute)
+    if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene)) != hipSuccess)
+      return e;
+  for (const void* f : half_cu)
+    if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kMaxLdsScene / 2))) !=
+        hipSuccess)
+      return e;
+  for (const void* f : whole_cu)
+    if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene)) != hipSuccess)
+      return e;
+  if (done.size() <= (size_t)device) done.resize((size_t)device + 1, 0);
+  done[(size_t)device] = 1;
+  return hipSuccess;
+}
+
 hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, int* ran, int* block_out) {
   TraceParams p = p0;
-  static bool lds_attr = false;
-  if (!lds_attr) {
-    lds_attr = true;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_brute_lds),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
-    const void* half_cu[] = {reinterpret_cast<const void*>(&trace_bundle_cull_lds<512, false>),
-                             reinterpret_cast<const void*>(&trace_bundle_cull_lds<512, true>)};
-    const void* whole_cu[] = {reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024, false>),
-                              reinterpret_cast<const void*>(&trace_bundle_cull_lds<1024, true>),
-                              reinterpret_cast<const void*>(&trace_bundle_bvh_lds<false>),
-                              reinterpret_cast<const void*>(&trace_bundle_bvh_lds<true>),
-                              reinterpret_cast<const void*>(&trace_bundle_wq<false>),
-                              reinterpret_cast<const void*>(&trace_bundle_wq<true>)};
-    for (const void* f : half_cu)
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kMaxLdsScene / 2));
-    for (const void* f : whole_cu)
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene);
-    (void)hipGetLastError();  // a refused attribute shows up as a launch failure of that kernel, not here
-  }
   variant = resolve_variant(p, variant);
   *ran = variant;
   // bounce batch threshold, auto: the pair traversal's step cost scales with its rays, so BUNDLE_WQ
@@ -2414,6 +2445,16 @@ hipError_t launch_accumulate(uint32_t* cur8, const uint32_t* new8, float4* cur32
     accumulate_rgba8<<<blocks_for(npix), 256, 0, stream>>>(cur8, new8, npix, frame);
   else
     accumulate_rgba32f<<<blocks_for(npix), 256, 0, stream>>>(cur32, new32, npix, frame);
+  return hipGetLastError();
+}
+
+hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint32_t row_words, uint32_t height,
+                                uint32_t local_rows, uint32_t row_tile, uint32_t parts, hipStream_t stream) {
+  if (row_words == 0 || height == 0) return hipSuccess;
+  if (parts == 0 || row_tile == 0 || (uint64_t)((height - 1) / row_tile / parts + 1) * row_tile > local_rows)
+    return hipErrorInvalidValue;  // some global row would read outside its part's local rows
+  const dim3 g(std::min<uint32_t>((row_words + 255) / 256, 64), height, 1);
+  assemble_rows<<<g, 256, 0, stream>>>(gathered, frame, row_words, local_rows, row_tile, parts);
   return hipGetLastError();
 }
 

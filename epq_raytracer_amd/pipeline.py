@@ -88,10 +88,12 @@ def sphere_records(spheres: List[Sphere]) -> np.ndarray:
 
 class HrtContext:
     """Owner of one hrt_context.  ``partition`` = (row_tile, part_index, part_count) selects the
-    interleaved row tiles this context renders (multi-GPU)."""
+    interleaved row tiles this context renders (multi-GPU).  ``debug=True`` binds
+    libhip_raytrace_debug.so (diagnostics-only options)."""
 
-    def __init__(self, image_size, device: int = -1, mode: int = _lib.MODE_RGBA8, partition=None):
-        self.lib = _lib.load()
+    def __init__(self, image_size, device: int = -1, mode: int = _lib.MODE_RGBA8, partition=None,
+                 debug: bool = False):
+        self.lib = _lib.load(debug)
         info = _lib.CreateInfo()
         info.width, info.height = int(image_size[0]), int(image_size[1])
         info.device = int(device)
@@ -101,10 +103,10 @@ class HrtContext:
         else:
             info.row_tile, info.part_index, info.part_count = 0, 0, 1
         h = ctypes.c_void_p()
-        _lib.check(self.lib.hrt_create(ctypes.byref(info), ctypes.byref(h)), "hrt_create")
+        _lib.check(self.lib.hrt_create(ctypes.byref(info), ctypes.byref(h)), "hrt_create", None, self.lib)
         self.handle = h
         lay = _lib.Layout()
-        _lib.check(self.lib.hrt_get_layout(self.handle, ctypes.byref(lay)), "hrt_get_layout", self.handle)
+        _lib.check(self.lib.hrt_get_layout(self.handle, ctypes.byref(lay)), "hrt_get_layout", self.handle, self.lib)
         self.width, self.height = lay.width, lay.height
         self.local_rows, self.row_tile = lay.local_rows, lay.row_tile
         self.part_index, self.part_count, self.mode = lay.part_index, lay.part_count, lay.mode
@@ -121,7 +123,7 @@ class HrtContext:
             pass
 
     def _check(self, st, where):
-        _lib.check(st, where, self.handle)
+        _lib.check(st, where, self.handle, self.lib)
 
     def set_scene(self, rays, spheres, tris, meshes):
         """rays=None keeps the context's rays (hrt_generate_rays or an earlier set_scene)."""
@@ -211,6 +213,53 @@ class HrtContext:
         """Copy into caller memory (host or device pointer, e.g. a torch tensor's data_ptr())."""
         self._check(self.lib.hrt_read_image(self.handle, image_id, fmt, ctypes.c_void_p(dst_ptr), nbytes),
                     "hrt_read_image")
+
+    def check_guards(self):
+        """libhip_raytrace_debug.so: (guarded device buffers, buffers whose guard bands were overwritten)."""
+        n, bad = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.lib.hrt_debug_check_guards(self.handle, ctypes.byref(n), ctypes.byref(bad)),
+                    "hrt_debug_check_guards")
+        return n.value, bad.value
+
+    # ---- multi-GPU framebuffer gather (hrt_comm_*) ----
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """A fresh RCCL unique id (rank 0 creates it and shares the bytes, e.g. by torch.distributed)."""
+        lib = _lib.load()
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+        _lib.check(lib.hrt_comm_unique_id(buf), "hrt_comm_unique_id", None, lib)
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes, rank: int, world: int):
+        """Join the RCCL communicator of a world-way partition (collective over the ranks)."""
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(uid)
+        self._check(self.lib.hrt_comm_init(self.handle, buf, int(rank), int(world)), "hrt_comm_init")
+
+    @staticmethod
+    def comm_init_all(ctxs):
+        """One process driving every part: ctxs[i] is part i of len(ctxs)."""
+        lib = ctxs[0].lib
+        arr = (ctypes.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+        _lib.check(lib.hrt_comm_init_all(arr, len(ctxs)), "hrt_comm_init_all", None, lib)
+
+    def comm_info(self):
+        """(rank, world, transport) of the context's communicator."""
+        r, w, t = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.lib.hrt_comm_info(self.handle, ctypes.byref(r), ctypes.byref(w), ctypes.byref(t)),
+                    "hrt_comm_info")
+        return r.value, w.value, t.value
+
+    def read_frame(self, image_id: int, fmt: int = _lib.FMT_RGBA8, root: bool = True):
+        """The gathered full frame (height, W, 4) through hrt_read_image on a context with a
+        communicator; ranks other than the root pass root=False and get None."""
+        if not root:
+            self._check(self.lib.hrt_read_image(self.handle, image_id, fmt, None, 0), "hrt_read_image")
+            return None
+        dt = np.uint8 if fmt == _lib.FMT_RGBA8 else np.float32
+        out = np.empty((self.height, self.width, 4), dtype=dt)
+        self._check(self.lib.hrt_read_image(self.handle, image_id, fmt, _lib.ptr(out), out.nbytes), "hrt_read_image")
+        return out
 
     def global_rows(self) -> np.ndarray:
         """Global row index of each local row (rows >= height are padding)."""

@@ -13,6 +13,7 @@
  *                    -> dispatch + push constants  src/raytrace_pipeline.rs:216-266
  *   hrt_accumulate   DiffusePipeline::next_frame src/diffuse.rs:73-101 (-> dispatch :103-136)
  *   hrt_read_image   RayTracePipeline::image / DiffusePipeline::image  src/raytrace_pipeline.rs:156, src/diffuse.rs:69
+ *                    (on a row-tile partition with a communicator: the RCCL framebuffer gather, hrt_comm_*)
  *   hrt_synchronize  then_signal_fence_and_flush().unwrap() + fence wait  src/raytrace_pipeline.rs:179-183
  *   hrt_last_error   the .unwrap() panics (every Vulkan call in src/raytrace_pipeline.rs / src/diffuse.rs)
  *
@@ -24,6 +25,9 @@
  * arrays are borrowed for the duration of the call only.  A context is NOT thread-safe: use it from
  * one host thread.  All work on a context is ordered on the context's own HIP stream
  * (== the reference's GpuFuture chaining); hrt_trace / hrt_accumulate return without waiting.
+ * Internally a trace runs on one of two trace lanes (own stream + trace image) so that frame k+1's
+ * trace overlaps frame k's tail; the combiner, reads and every other call stay in call order on the
+ * context's stream, so results equal the serial loop's byte for byte (HRT_OPT_OVERLAP).
  */
 #ifndef HIP_RAYTRACE_H
 #define HIP_RAYTRACE_H
@@ -197,9 +201,11 @@ typedef enum hrt_option {
    * auto: BUNDLE_WQ 2; the others 3 when there are more than 4 tiles per resident wave, else 1) */
   HRT_OPT_SPLIT_FACTOR = 6,
   /* persistent kernels: heavy tiles (as above) run at raised wave issue priority (1 default, 0 off;
-   * 2 = diagnostics: a planned trace runs ONLY the heavy tiles, the frame is incomplete) */
+   * libhip_raytrace_debug.so only: 2 = a planned trace runs ONLY the heavy tiles, the frame is
+   * incomplete -- a diagnostics mode the production library rejects) */
   HRT_OPT_PRIORITY = 7,
-  /* persistent kernels: launch workgroups for at most this many CUs (0 = all; latency experiments) */
+  /* libhip_raytrace_debug.so only (latency experiments): persistent kernels launch workgroups for at
+   * most this many CUs (0 = all).  The production library rejects the key. */
   HRT_OPT_GRID_CUS = 8,
   /* BUNDLE_CULL_LDS with HRT_OPT_SPLIT = 1: heavy tiles run cooperatively, every wave of a workgroup
    * on the same tile with the bounce cull's chunks dealt out over the waves (1 default, 0 off) */
@@ -214,7 +220,14 @@ typedef enum hrt_option {
   HRT_OPT_PROBE = 11,
   /* hrt_compute_n: frames traced by one persistent launch (default 64, 1 = one launch per frame;
    * also capped at 1 GiB of frame images).  Results do not depend on it. */
-  HRT_OPT_FRAMES_PER_LAUNCH = 12
+  HRT_OPT_FRAMES_PER_LAUNCH = 12,
+  /* hrt_trace: consecutive traces alternate between two trace lanes so that the next frame's trace
+   * starts while the current one finishes (1 default; 0 = one lane, each trace after the previous
+   * frame's combiner).  Results do not depend on it.  Diagnostics (HRT_OPT_COUNTERS = 2) use one lane. */
+  HRT_OPT_OVERLAP = 13,
+  /* libhip_raytrace_debug.so only (tests): the value-th device allocation of the next hrt_set_scene
+   * fails with HRT_ERR_OUT_OF_MEMORY (0 = off) */
+  HRT_DEBUG_OPT_FAIL_ALLOC = 1001
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */
@@ -255,6 +268,15 @@ typedef enum hrt_scene_info {
 } hrt_scene_info;
 
 uint32_t hrt_abi_version(void);
+/* Identity of the device code (hash of the kernel sources and build flags): measurement records
+ * (profiles/pmc_traffic.json) carry it, so counters of an older kernel are never applied to this one. */
+const char* hrt_build_id(void);
+/* 1 for libhip_raytrace_debug.so (accepts the debug-only options above), 0 for the production library. */
+uint32_t hrt_debug_build(void);
+/* libhip_raytrace_debug.so: every device buffer of the context is surrounded by 4 KiB guard bands of a
+ * fixed pattern; this synchronizes and counts the buffers and those whose bands were overwritten (a
+ * kernel wrote outside its buffer).  The production library returns HRT_ERR_INVALID_ARGUMENT. */
+hrt_status hrt_debug_check_guards(hrt_context* ctx, uint32_t* buffers, uint32_t* corrupted);
 
 hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_ctx);
 void hrt_destroy(hrt_context* ctx);
@@ -283,9 +305,31 @@ hrt_status hrt_accumulate(hrt_context* ctx, uint32_t frame);
  * frame alone; the combiner then folds the frames in order.  pc->init must be 0. */
 hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* pc, uint32_t n);
 
-/* Copy this context's local rows of an image (row-major, local_rows x width x 4 channels) into dst,
- * which may be host or device memory.  Blocking.  bytes must be >= the image size in fmt. */
+/* Copy an image (row-major, x 4 channels) into dst, host or device memory.  Blocking.
+ *  - Without a communicator: this context's local rows (local_rows x width); bytes >= that in fmt.
+ *  - With one (hrt_comm_init / hrt_comm_init_all): the FULL frame (height x width), gathered from every
+ *    part with one ncclGather to rank 0 and un-interleaved on rank 0's device.  hrt_comm_init: a
+ *    collective -- every rank calls it; dst / bytes are used on rank 0 only (may be NULL elsewhere).
+ *    hrt_comm_init_all: any context of the group may call it alone; the frame lands in dst. */
 hrt_status hrt_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes);
+
+/* ---- multi-GPU framebuffer gather (RCCL is loaded on first use) ------------------- */
+#define HRT_COMM_ID_BYTES 128 /* == sizeof(ncclUniqueId) */
+typedef enum hrt_comm_transport {
+  HRT_COMM_NONE = 0,        /* no communicator */
+  HRT_COMM_RCCL = 1,        /* hrt_comm_init: one process / thread per GPU, ncclCommInitRank */
+  HRT_COMM_RCCL_GROUP = 2,  /* hrt_comm_init_all on distinct devices: ncclCommInitAll, grouped ncclGather */
+  HRT_COMM_DEVICE_COPY = 3  /* hrt_comm_init_all with contexts sharing a device: device-to-device copies */
+} hrt_comm_transport;
+/* A fresh RCCL unique id (ncclGetUniqueId) for hrt_comm_init; rank 0 creates it and shares the bytes. */
+hrt_status hrt_comm_unique_id(uint8_t id[HRT_COMM_ID_BYTES]);
+/* Joins ctx -- part `rank` of a `world`-way row-tile partition (hrt_create_info), or the whole image
+ * when world == 1 -- to the communicator named by id.  Collective: blocks until all ranks joined. */
+hrt_status hrt_comm_init(hrt_context* ctx, const uint8_t id[HRT_COMM_ID_BYTES], uint32_t rank, uint32_t world);
+/* One process driving every part: ctxs[i] must be part i of n (same size, mode, row tile). */
+hrt_status hrt_comm_init_all(hrt_context* const* ctxs, uint32_t n);
+/* rank / world / hrt_comm_transport of ctx's communicator (0 / 1 / HRT_COMM_NONE without one). */
+hrt_status hrt_comm_info(const hrt_context* ctx, uint32_t* rank, uint32_t* world, uint32_t* transport);
 
 hrt_status hrt_get_layout(const hrt_context* ctx, hrt_layout* out);
 hrt_status hrt_synchronize(hrt_context* ctx);
@@ -325,7 +369,8 @@ hrt_status hrt_debug_export_memory(int device, uint64_t bytes, int* fd, void** p
 hrt_status hrt_debug_unmap_memory(void* ptr, uint64_t size);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
-/* HIP stream the context's work is ordered on (hipStream_t), for callers that interoperate. */
+/* The context's HIP stream (hipStream_t), for callers that interoperate: work enqueued on it after
+ * hrt_accumulate / hrt_compute_n follows them (a trace is joined by the combiner that reads it). */
 void* hrt_stream(hrt_context* ctx);
 
 /* Text of the last error on ctx (or of the last hrt_create failure when ctx is NULL). */

@@ -33,6 +33,22 @@ def build() -> None:
 
 
 _lib = None
+_variants = {}
+
+# Parity-risk variants (rt_oracle.c header): driver-typical numerics, never the checker.
+DRIVER_VARIANTS = ("math", "rsq", "contract", "all")
+
+
+def load_driver_variant(name: str) -> ctypes.CDLL:
+    """liborc_drv_<name>.so: the oracle with one driver-typical numerics choice (needs FMA hardware)."""
+    if name not in DRIVER_VARIANTS:
+        raise ValueError(name)
+    if name not in _variants:
+        path = os.path.join(BUILD, f"liborc_drv_{name}.so")
+        if not os.path.exists(path):
+            build()
+        _variants[name] = _bind(ctypes.CDLL(path))
+    return _variants[name]
 
 
 def load(prefer_fma: bool | None = None) -> ctypes.CDLL:
@@ -45,7 +61,11 @@ def load(prefer_fma: bool | None = None) -> ctypes.CDLL:
     path = os.path.join(BUILD, "liborc_fma.so" if fma else "liborc.so")
     if not os.path.exists(path):
         build()
-    lib = ctypes.CDLL(path)
+    _lib = _bind(ctypes.CDLL(path))
+    return _lib
+
+
+def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
     P = c_void_p
     lib.orc_hash_step.restype = c_uint32
     lib.orc_hash_step.argtypes = [POINTER(c_uint32)]
@@ -79,8 +99,9 @@ def load(prefer_fma: bool | None = None) -> ctypes.CDLL:
     lib.orc_create_rays.argtypes = [c_uint32, c_uint32, c_float, c_float, P, P, POINTER(c_float)]
     lib.orc_transform_mesh.restype = None
     lib.orc_transform_mesh.argtypes = [P, P, c_uint32, P, P, P]
+    lib.orc_trace_pixels.restype = None
+    lib.orc_trace_pixels.argtypes = [P, P, P, P, P, P, c_uint32, P, POINTER(c_uint64), POINTER(c_uint64), c_int]
     lib.orc_num_threads.restype = c_int
-    _lib = lib
     return lib
 
 
@@ -194,11 +215,11 @@ def transform_meshes(meshes, tri_dtype, mesh_dtype, material_dtype):
 
 # ---- trace / accumulate ------------------------------------------------------------------------
 
-def trace(pc, rays, spheres, tris, meshes, rows=None, nthreads: int = 0, want_f32: bool = False):
+def trace(pc, rays, spheres, tris, meshes, rows=None, nthreads: int = 0, want_f32: bool = False, lib=None):
     """Trace the full frame (or global rows [y0, y1)).  pc: a 124-byte ctypes PushConstants.
     Returns (rgba8 (H, W, 4) uint8, rgba32f or None, segments, tri_tests); rows outside the range
-    are left zero."""
-    lib = load()
+    are left zero.  lib: a load_driver_variant() library instead of the pinned oracle."""
+    lib = lib or load()
     W, H = pc.width, pc.height
     y0, y1 = (0, H) if rows is None else rows
     img8 = np.zeros((H, W, 4), np.uint8)
@@ -208,6 +229,18 @@ def trace(pc, rays, spheres, tris, meshes, rows=None, nthreads: int = 0, want_f3
     lib.orc_trace_rows(ctypes.byref(pc), *[_p(a) for a in keep], y0, y1, _p(img8), _p(img32), ctypes.byref(seg),
                        ctypes.byref(tt), int(nthreads))
     return img8, img32, seg.value, tt.value
+
+
+def trace_pixels(pc, rays, spheres, tris, meshes, xs, ys, nthreads: int = 0):
+    """rgba8 (n, 4) of the listed pixels of one frame, plus the exact segment / triangle-test counts."""
+    xy = np.ascontiguousarray(np.stack([np.asarray(xs, np.uint32), np.asarray(ys, np.uint32)], -1).reshape(-1))
+    n = len(xy) // 2
+    out = np.zeros((n, 4), np.uint8)
+    seg, tt = c_uint64(), c_uint64()
+    keep = [np.ascontiguousarray(rays).view(np.uint8), _bytes(spheres), _bytes(tris), _bytes(meshes)]
+    load().orc_trace_pixels(ctypes.byref(pc), *[_p(a) for a in keep], _p(xy), n, _p(out), ctypes.byref(seg),
+                            ctypes.byref(tt), int(nthreads))
+    return out, seg.value, tt.value
 
 
 def trace_pixel(pc, rays, spheres, tris, meshes, x: int, y: int):

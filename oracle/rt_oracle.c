@@ -33,6 +33,14 @@
  *       a.y*b.z - a.z*b.y ..., magnitude = sqrt((x*x + y*y) + z*z), normalised = v / magnitude.
  *
  * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fno-fast-math -fopenmp).
+ *
+ * Parity-risk variants (oracle/Makefile liborc_drv_*.so; tests/test_parity_risk.py):
+ * what a Vulkan driver typically emits where the GLSL leaves the choice open, one choice at a time --
+ *   ORC_DRIVER_MATH      log/sin/cos from the C library (glibc logf/sinf/cosf) instead of S5;
+ *   ORC_DRIVER_RSQ       normalize(v) = v * (1/sqrt(dot(v,v))) instead of S4's three divides;
+ *   -ffp-contract=fast   the compiler fuses a*b+c wherever it likes (instead of S3).
+ * They measure how far "bit-exact against this oracle" can sit from a real driver's frame; they
+ * are never the checker.
  */
 #include <math.h>
 #include <stdint.h>
@@ -88,7 +96,11 @@ static inline v3 cross3(v3 a, v3 b) {
   return mk3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
 }
 /* S4 */
+#ifdef ORC_DRIVER_RSQ
+static inline v3 normalize3(v3 a) { float r = 1.0f / sqrtf(dot3(a, a)); return muls3(a, r); }
+#else
 static inline v3 normalize3(v3 a) { float l = sqrtf(dot3(a, a)); return divs3(a, l); }
+#endif
 /* S6 */
 static inline float glsl_min(float x, float y) { return (y < x) ? y : x; }
 static inline float glsl_max(float x, float y) { return (x < y) ? y : x; }
@@ -175,6 +187,16 @@ float spec_cosf(float x) {
   }
 }
 
+#ifdef ORC_DRIVER_MATH
+#define ORC_LOGF logf
+#define ORC_SINF sinf
+#define ORC_COSF cosf
+#else
+#define ORC_LOGF spec_logf
+#define ORC_SINF spec_sinf
+#define ORC_COSF spec_cosf
+#endif
+
 /* ---------------------------------------------------------------------------------
  * RNG -- assets/raytracing.glsl:13-40
  * ------------------------------------------------------------------------------- */
@@ -195,8 +217,8 @@ static inline float orc_u01(uint32_t s) { return (float)s / 4294967296.0f; }
 /* RandomValueNormalDistribution, raytracing.glsl:28-33 (u1 then u2) */
 static inline float orc_normal(uint32_t* state) {
   float theta = 6.2831852f * orc_u01(orc_hash(state)); /* 2 * 3.1415926, folded exactly */
-  float rho = sqrtf(-2.0f * spec_logf(orc_u01(orc_hash(state))));
-  return rho * spec_cosf(theta);
+  float rho = sqrtf(-2.0f * ORC_LOGF(orc_u01(orc_hash(state))));
+  return rho * ORC_COSF(theta);
 }
 /* RandomPointOnUnitSphere, raytracing.glsl:35-40 (x, y, z order) */
 static inline v3 orc_unit_sphere(uint32_t* state) {
@@ -392,11 +414,11 @@ static v3 trace_ray(orc_world* w, const orc_push* pc, v3 root, v3 dir, uint32_t*
 /* get_ray_dir, raytracing.glsl:162-166 (u1, u2, u3 in order; left-to-right evaluation) */
 static inline v3 get_ray_dir(const orc_push* pc, v3 c, uint32_t* state) {
   float r = (orc_u01(orc_hash(state)) * 2.0f) * 3.14159265358979323846f;
-  float cr = spec_cosf(r);
+  float cr = ORC_COSF(r);
   float j = pc->jitter_size;
   float s2 = sqrtf(orc_u01(orc_hash(state)));
   v3 t1 = muls3(muls3(muls3(mk3(0.0f, 0.0f, 1.0f), cr), j), s2);
-  float sr = spec_sinf(r);
+  float sr = ORC_SINF(r);
   float s3 = sqrtf(orc_u01(orc_hash(state)));
   v3 t2 = muls3(muls3(muls3(mk3(0.0f, 1.0f, 0.0f), sr), j), s3);
   v3 nc = add3(add3(c, t1), t2);
@@ -487,6 +509,29 @@ void orc_trace_pixel(const orc_push* pc, const orc_ray* rays, const orc_sphere* 
   shade_pixel(&w, pc, rays, x, y, out_rgb);
   if (segments) *segments = w.segments;
   if (tri_tests) *tri_tests = w.tri_tests;
+}
+
+/* A list of pixels (xy[2k], xy[2k+1]) of one frame: rgba8 out[4k..4k+3] (OpenMP over the list). */
+void orc_trace_pixels(const orc_push* pc, const orc_ray* rays, const orc_sphere* spheres,
+                      const orc_triangle* tris, const orc_mesh* meshes, const uint32_t* xy, uint32_t n,
+                      uint8_t* out, uint64_t* segments, uint64_t* tri_tests, int nthreads) {
+  uint64_t seg = 0, tt = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+  (void)nthreads;
+#endif
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : seg, tt)
+  for (long k = 0; k < (long)n; k++) {
+    orc_world w = {spheres, pc->num_spheres, tris, meshes, pc->num_meshes, 0, 0};
+    float rgb[3];
+    shade_pixel(&w, pc, rays, xy[2 * k], xy[2 * k + 1], rgb);
+    out[4 * k] = unorm8(rgb[0]); out[4 * k + 1] = unorm8(rgb[1]);
+    out[4 * k + 2] = unorm8(rgb[2]); out[4 * k + 3] = 255;
+    seg += w.segments; tt += w.tri_tests;
+  }
+  if (segments) *segments = seg;
+  if (tri_tests) *tri_tests = tt;
 }
 
 /* image_combiner.glsl:22-43 on rgba8 images (npix pixels). */

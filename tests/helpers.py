@@ -54,9 +54,11 @@ class SceneCase:
         return pyoracle.trace(self.push(rng_offset), self.rays, self.spheres, self.tris, self.meshes, rows=rows,
                               nthreads=nthreads, want_f32=want_f32)
 
-    def context(self, mode=_lib.MODE_RGBA8, partition=None, variant=0, device=0, options=None):  # noqa: PLR0913
-        """options: {hrt_option: value} applied before set_scene (e.g. the BVH leaf size)."""
-        ctx = E.HrtContext(self.size, device=device, mode=mode, partition=partition)
+    def context(self, mode=_lib.MODE_RGBA8, partition=None, variant=0, device=0, options=None,  # noqa: PLR0913
+                debug=False):
+        """options: {hrt_option: value} applied before set_scene (e.g. the BVH leaf size); debug binds
+        libhip_raytrace_debug.so (diagnostics-only options, guard bands)."""
+        ctx = E.HrtContext(self.size, device=device, mode=mode, partition=partition, debug=debug)
         ctx.set_option(_lib.OPT_KERNEL_VARIANT, variant)
         for k, v in (options or {}).items():
             ctx.set_option(k, v)

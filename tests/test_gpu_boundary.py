@@ -1,0 +1,263 @@
+"""GPU tests of the drop-in boundary added in round 2 (include/hip_raytrace.h):
+
+* trace lanes (HRT_OPT_OVERLAP): the realtime loop's consecutive traces overlap; frames, accumulator
+  and counters must equal the serial loop and hrt_compute_n byte for byte, with reads interleaved;
+* the framebuffer gather behind hrt_read_image (hrt_comm_*): device-copy groups on one GPU (the
+  un-interleave kernel against rowtiles.assembly_index), and RCCL communicators of one rank;
+* libhip_raytrace_debug.so: guard bands around every device buffer after traces at ragged sizes,
+  and a failed hrt_set_scene (injected allocation failure) leaving the previous scene intact;
+* the production library rejecting the diagnostics-only options.
+"""
+import numpy as np
+import pytest
+
+import pyoracle
+from helpers import E, SceneCase, _lib, mismatch_report
+from epq_raytracer_amd import rowtiles
+
+pytestmark = pytest.mark.gpu
+
+
+def _loop(case, frames, first=1, overlap=1, variant=0, mode=_lib.MODE_RGBA8, read_each=False, partition=None,
+          debug=False):
+    ctx = E.HrtContext(case.size, device=0, mode=mode, partition=partition, debug=debug)
+    ctx.set_option(_lib.OPT_KERNEL_VARIANT, variant)
+    ctx.set_option(_lib.OPT_OVERLAP, overlap)
+    ctx.set_scene(case.rays, case.spheres, case.tris, case.meshes)
+    fmt = _lib.FMT_RGBA8 if mode == _lib.MODE_RGBA8 else _lib.FMT_RGBA32F
+    traces = []
+    for k in range(first, first + frames):
+        ctx.trace(case.push(k))
+        if read_each:
+            traces.append(ctx.read(_lib.IMG_TRACE, fmt))
+        ctx.accumulate(k)
+    st = ctx.stats()
+    out = ctx.read(_lib.IMG_ACCUM, fmt), ctx.read(_lib.IMG_TRACE, fmt), st, traces
+    return ctx, out
+
+
+@pytest.mark.parametrize("scene,size,spp,variant,mode", [
+    ("island", (96, 64), 3, 9, _lib.MODE_RGBA8),
+    ("island", (256, 256), 1, 0, _lib.MODE_RGBA8),      # probe-planned first trace on each lane
+    ("cave", (64, 48), 2, 7, _lib.MODE_RGBA32F),
+    ("box", (45, 33), 3, 5, _lib.MODE_RGBA8),           # non-persistent kernel on the lanes
+])
+def test_overlapped_realtime_loop_is_byte_exact(scene, size, spp, variant, mode):
+    """compute_then_render per frame (src/raytracing_app.rs:156-194) with the traces alternating
+    between two lanes == the same loop on one lane == hrt_compute_n, byte for byte."""
+    case = SceneCase(scene, size, spp, 8)
+    n = 6
+    results = []
+    for overlap in (1, 0):
+        ctx, r = _loop(case, n, first=2, overlap=overlap, variant=variant, mode=mode)
+        ctx.close()
+        results.append(r)
+    ctx = case.context(mode=mode, variant=variant)
+    ctx.compute_n(case.push(2), n)
+    fmt = _lib.FMT_RGBA8 if mode == _lib.MODE_RGBA8 else _lib.FMT_RGBA32F
+    batched = ctx.read(_lib.IMG_ACCUM, fmt), ctx.read(_lib.IMG_TRACE, fmt), ctx.stats()
+    ctx.close()
+    for acc, trace, st, _ in results:
+        assert np.array_equal(acc.view(np.uint8), batched[0].view(np.uint8))
+        assert np.array_equal(trace.view(np.uint8), batched[1].view(np.uint8))
+        assert (st.segments, st.tri_tests, st.traces, st.accumulates) == \
+            (batched[2].segments, batched[2].tri_tests, batched[2].traces, batched[2].accumulates)
+
+
+def test_overlapped_traces_read_back_in_order():
+    """Every trace image read between overlapped traces is that frame's oracle frame."""
+    case = SceneCase("island", (80, 48), 2, 8)
+    ctx, (_, _, _, traces) = _loop(case, 4, first=1, overlap=1, read_each=True)
+    ctx.close()
+    for k, img in enumerate(traces, start=1):
+        ref = case.oracle(rng_offset=k)[0]
+        assert np.array_equal(img, ref), f"frame {k}: " + mismatch_report(img, ref)
+
+
+def test_overlap_then_compute_n_then_overlap():
+    """Lanes and hrt_compute_n interleaved on one context: the accumulator equals one serial loop."""
+    case = SceneCase("island", (96, 64), 2, 8)
+    ref_ctx, (want, want_trace, _, _) = _loop(case, 9, first=1, overlap=0)
+    ref_ctx.close()
+    ctx = case.context()
+    for k in (1, 2):
+        ctx.trace(case.push(k))
+        ctx.accumulate(k)
+    ctx.compute_n(case.push(3), 4)
+    for k in (7, 8, 9):
+        ctx.trace(case.push(k))
+        ctx.accumulate(k)
+    got, got_trace = ctx.read(_lib.IMG_ACCUM), ctx.read(_lib.IMG_TRACE)
+    ctx.close()
+    assert np.array_equal(got, want) and np.array_equal(got_trace, want_trace)
+
+
+# ---- framebuffer gather (hrt_comm_*) -----------------------------------------------------------
+
+@pytest.mark.parametrize("parts,tile", [(2, 8), (3, 16), (8, 8), (5, 4)])
+def test_gather_device_copy_group(parts, tile):
+    """hrt_comm_init_all over parts contexts sharing device 0 (HRT_COMM_DEVICE_COPY): hrt_read_image
+    returns the full frame, equal to rowtiles.assembly_index over the parts' local rows, to the
+    unpartitioned frame and (trace image) to the oracle; rgba32f reads convert the gathered frame."""
+    case = SceneCase("island", (80, 70), 2, 8)
+    ref = case.oracle(rng_offset=2)[0]
+    full_ctx, (want_acc, want_trace, _, _) = _loop(case, 2, first=1)
+    want_acc32 = full_ctx.read(_lib.IMG_ACCUM, _lib.FMT_RGBA32F)
+    full_ctx.close()
+    ctxs = []
+    for p in range(parts):
+        c, _ = _loop(case, 2, first=1, partition=(tile, p, parts))
+        ctxs.append(c)
+    local = [c.read(_lib.IMG_ACCUM) for c in ctxs]
+    E.HrtContext.comm_init_all(ctxs)
+    assert ctxs[1].comm_info() == (1, parts, _lib.COMM_DEVICE_COPY)
+    host = np.concatenate(local)[rowtiles.assembly_index(70, tile, parts)]
+    for c in (ctxs[0], ctxs[-1]):  # any member may read the group's frame
+        got = c.read_frame(_lib.IMG_ACCUM)
+        assert np.array_equal(got, host), mismatch_report(got, host)
+        assert np.array_equal(got, want_acc)
+    assert np.array_equal(ctxs[0].read_frame(_lib.IMG_TRACE), ref)
+    assert np.array_equal(ctxs[0].read_frame(_lib.IMG_TRACE), want_trace)
+    np.testing.assert_array_equal(ctxs[0].read_frame(_lib.IMG_ACCUM, _lib.FMT_RGBA32F).view(np.uint32),
+                                  want_acc32.view(np.uint32))
+    # the parts keep rendering after a gather (the members' streams wait for the copies)
+    for c in ctxs:
+        c.trace(case.push(3))
+        c.accumulate(3)
+    got3 = ctxs[0].read_frame(_lib.IMG_TRACE)
+    assert np.array_equal(got3, case.oracle(rng_offset=3)[0])
+    ctxs[1].close()
+    with pytest.raises(_lib.HrtError, match="destroyed"):
+        ctxs[0].read_frame(_lib.IMG_ACCUM)
+    for c in ctxs:
+        c.close()
+
+
+def test_gather_rccl_single_rank():
+    """The RCCL paths with one rank (all a one-GPU box can form): hrt_comm_init (ncclCommInitRank +
+    ncclGather to rank 0) and hrt_comm_init_all (ncclCommInitAll + grouped ncclGather) return the
+    frame the context holds."""
+    case = SceneCase("box", (64, 48), 2, 4)
+    for mode in ("rank", "all"):
+        ctx, (want_acc, want_trace, _, _) = _loop(case, 3)
+        if mode == "rank":
+            ctx.comm_init(E.HrtContext.comm_unique_id(), 0, 1)
+            assert ctx.comm_info() == (0, 1, _lib.COMM_RCCL)
+        else:
+            E.HrtContext.comm_init_all([ctx])
+            assert ctx.comm_info() == (0, 1, _lib.COMM_RCCL_GROUP)
+        assert np.array_equal(ctx.read_frame(_lib.IMG_ACCUM), want_acc)
+        assert np.array_equal(ctx.read_frame(_lib.IMG_TRACE), want_trace)
+        ctx.trace(case.push(4))  # a trace after the gather
+        assert np.array_equal(ctx.read_frame(_lib.IMG_TRACE), case.oracle(rng_offset=4)[0])
+        ctx.close()
+
+
+def test_comm_arguments_validated():
+    case = SceneCase("box", (32, 32), 1, 1)
+    a = case.context(partition=(8, 0, 2))
+    b = case.context(partition=(8, 1, 2))
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        E.HrtContext.comm_init_all([b, a])  # ctxs[i] must be part i
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        a.comm_init(bytes(_lib.COMM_ID_BYTES), 1, 2)  # rank differs from the partition
+    full = case.context()
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        E.HrtContext.comm_init_all([full, b])
+    E.HrtContext.comm_init_all([a, b])
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        E.HrtContext.comm_init_all([a, b])  # already in a group
+    with pytest.raises(_lib.HrtError, match="INVALID"):  # the gathered frame is the full 32 x 32
+        a.read_into(_lib.IMG_ACCUM, _lib.FMT_RGBA8, np.zeros(16 * 32 * 4, np.uint8).ctypes.data, 16 * 32 * 4)
+    for c in (a, b, full):
+        c.close()
+
+
+# ---- libhip_raytrace_debug.so: guard bands, injected failures ---------------------------------
+
+@pytest.mark.parametrize("scene,size,spp,partition", [
+    ("box", (37, 23), 3, None), ("island", (300, 1), 2, None), ("island", (1, 130), 2, None),
+    ("cave", (75, 41), 2, (8, 1, 3)), ("island", (129, 67), 2, (4, 2, 3)), ("spheres", (33, 65), 2, None),
+])
+def test_guard_bands_intact_after_traces(scene, size, spp, partition):
+    """Every device buffer (trace / accumulate images of both lanes, frame stack, camera lists, BVH
+    and band lists, planner buffers, counters, gather buffers) sits between 4 KiB guard bands in the
+    debug library; after every variant, compute_n batches, overlapped loops and a gather at ragged
+    sizes none of the bands has changed."""
+    case = SceneCase(scene, size, spp, 8)
+    ctx = E.HrtContext(size, device=0, partition=partition, debug=True)
+    assert ctx.lib.hrt_debug_build() == 1
+    ctx.set_option(_lib.OPT_COUNTERS, 2)  # tile profile buffer too
+    ctx.set_scene(case.rays, case.spheres, case.tris, case.meshes)
+    for v in range(10):
+        ctx.set_option(_lib.OPT_KERNEL_VARIANT, v)
+        ctx.trace(case.push(v + 1))
+        ctx.accumulate(v + 1)
+    ctx.set_option(_lib.OPT_COUNTERS, 1)
+    ctx.set_option(_lib.OPT_KERNEL_VARIANT, 0)
+    ctx.set_option(_lib.OPT_FRAMES_PER_LAUNCH, 3)
+    ctx.compute_n(case.push(20), 7)
+    for k in range(30, 34):
+        ctx.trace(case.push(k))
+        ctx.accumulate(k)
+    if partition is None:
+        ctx.comm_init(E.HrtContext.comm_unique_id(), 0, 1)
+        ctx.read_frame(_lib.IMG_ACCUM, _lib.FMT_RGBA32F)
+    n, bad = ctx.check_guards()
+    ctx.close()
+    assert n >= 20 and bad == 0, (n, bad)
+
+
+def test_failed_set_scene_keeps_the_previous_scene():
+    """a failure inside hrt_set_scene (here the k-th device allocation, injected through
+    libhip_raytrace_debug.so) must not leave stale counts next to freed buffers: the call reports
+    HRT_ERR_OUT_OF_MEMORY and the previous scene still traces byte for byte."""
+    box = SceneCase("box", (48, 40), 2, 4)
+    island = SceneCase("island", (48, 40), 2, 8)
+    ref = box.oracle()[0]
+    ctx = E.HrtContext(box.size, device=0, debug=True)
+    ctx.set_scene(box.rays, box.spheres, box.tris, box.meshes)
+    k = 1
+    while True:
+        ctx.set_option(_lib.DEBUG_OPT_FAIL_ALLOC, k)
+        try:
+            ctx.set_scene(island.rays, island.spheres, island.tris, island.meshes)
+            break  # fewer than k allocations: the injection did not fire, the scene is island now
+        except _lib.HrtError as e:
+            assert "OUT_OF_MEMORY" in str(e), e
+        ctx.trace(box.push())
+        assert np.array_equal(ctx.read(_lib.IMG_TRACE), ref), f"allocation {k}"
+        k += 1
+    assert k > 10  # rays, records, camera lists of both lanes, hierarchy, band lists ...
+    ctx.trace(island.push())
+    assert np.array_equal(ctx.read(_lib.IMG_TRACE), island.oracle()[0])
+    n, bad = ctx.check_guards()
+    assert bad == 0
+    ctx.close()
+    fresh = E.HrtContext(box.size, device=0, debug=True)
+    fresh.set_option(_lib.DEBUG_OPT_FAIL_ALLOC, 3)
+    with pytest.raises(_lib.HrtError, match="OUT_OF_MEMORY"):
+        fresh.set_scene(box.rays, box.spheres, box.tris, box.meshes)
+    with pytest.raises(_lib.HrtError, match="NO_SCENE"):
+        fresh.trace(box.push())
+    fresh.close()
+
+
+def test_production_library_rejects_debug_options():
+    case = SceneCase("box", (16, 16), 1, 1)
+    ctx = case.context()
+    assert ctx.lib.hrt_debug_build() == 0
+    for key, value in ((_lib.OPT_PRIORITY, 2), (_lib.OPT_GRID_CUS, 4), (_lib.DEBUG_OPT_FAIL_ALLOC, 1)):
+        with pytest.raises(_lib.HrtError, match="INVALID"):
+            ctx.set_option(key, value)
+    ctx.set_option(_lib.OPT_PRIORITY, 0)
+    with pytest.raises(_lib.HrtError, match="INVALID"):
+        ctx.check_guards()
+    for bad in (-1, 2):
+        with pytest.raises(_lib.HrtError, match="INVALID"):
+            ctx.set_option(_lib.OPT_OVERLAP, bad)
+    ctx.close()
+    dbg = E.HrtContext((16, 16), device=0, debug=True)
+    dbg.set_option(_lib.OPT_PRIORITY, 2)
+    dbg.set_option(_lib.OPT_GRID_CUS, 4)
+    dbg.close()

@@ -40,7 +40,8 @@ def main():
                        options={_lib.OPT_COOP: a.coop, _lib.OPT_SPLIT_FACTOR: a.factor, _lib.OPT_PRIORITY: a.prio,
                                 _lib.OPT_SPLIT: a.split, _lib.OPT_SECONDARY_BATCH: a.sec_batch,
                                 _lib.OPT_WQ_NODE_CAP: a.ncap, _lib.OPT_PROBE: a.probe,
-                                **({_lib.OPT_BVH_LEAF_SIZE: a.leaf} if a.leaf > 0 else {})})
+                                **({_lib.OPT_BVH_LEAF_SIZE: a.leaf} if a.leaf > 0 else {})},
+                       debug=a.prio == 2)  # heavy tiles only: a libhip_raytrace_debug.so diagnostics mode
     pc = case.push(1)
     ms = []
     if a.batch > 0:

@@ -1,13 +1,13 @@
 #!/bin/bash
-# PMC passes for one kbench variant, each pass its own rocprofv3 run (--pmc with --kernel-trace only).
-# Usage: bash tools/pmc.sh <tag> <variant> [--scene S --size WxH --spp N --bounces B]
-# Writes gpurun_out/<tag>/summary.json and gpurun_out/<tag>/pmc_traffic.json (bench.py's `traffic`).
+# PMC passes of the bench command itself (so the profiled launch is the timed launch: one hrt_compute_n
+# launch of STEPS frames after the warm-up), each pass its own rocprofv3 run (--pmc with --kernel-trace
+# only).  Usage: bash tools/pmc.sh <tag> [bench.py args...]   (default: the headline, 64 frames)
+# Writes gpurun_out/<tag>/summary.json and gpurun_out/<tag>/pmc_traffic.json (bench.py's roofline).
 set -o pipefail
-TAG=$1; V=$2; shift 2
+TAG=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 OUT=gpurun_out/$TAG; mkdir -p $OUT
-SCENE=island; SIZE=1920x1080; SPP=64; BOUNCES=8
-while [ $# -gt 0 ]; do case $1 in --scene) SCENE=$2;; --size) SIZE=$2;; --spp) SPP=$2;; --bounces) BOUNCES=$2;; esac; shift 2; done
+ARGS="--warmup 2 --steps 64 --cpu-seconds 0 $*"
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
@@ -15,10 +15,17 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" \
            "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_LDS_BANK_CONFLICT"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- \
-    python3 tools/kbench.py --no-ref --variants $V --rounds 1 --scene $SCENE --size $SIZE --spp $SPP --bounces $BOUNCES \
-    > $OUT/p$i.log 2>&1 || { echo "pass $i ($set) failed: $(tail -3 $OUT/p$i.log)"; exit 1; }
+    python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i ($set) failed: $(tail -3 $OUT/p$i.log)"; exit 1; }
 done
-W=${SIZE%x*}; H=${SIZE#*x}
-python3 tools/pmc_summary.py $OUT --traffic-json $OUT/pmc_traffic.json \
-  --workload scene=$SCENE width=$W height=$H spp=$SPP bounces=$BOUNCES variant=$V > $OUT/summary.json
+WL=$(python3 - "$OUT/p1.log" <<'PY'
+import json, sys
+for line in open(sys.argv[1]):
+    if line.startswith("{"):
+        c = json.loads(line)["config"]
+        print(" ".join(f"{k}={c[k]}" for k in ("scene", "width", "height", "spp", "bounces", "kernel_variant",
+                                                 "frames_per_launch")), json.loads(line)["steps"])
+PY
+)
+FRAMES=${WL##* }; WL=${WL% *}
+python3 tools/pmc_summary.py $OUT --traffic-json $OUT/pmc_traffic.json --frames $FRAMES --workload $WL > $OUT/summary.json
 cat $OUT/pmc_traffic.json

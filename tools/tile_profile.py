@@ -33,7 +33,7 @@ def main():
     W, H = (int(v) for v in a.size.split("x"))
     case = SceneCase(a.scene, (W, H), a.spp, a.bounces)
     part = tuple(int(v) for v in a.partition.split(",")) if a.partition else None
-    ctx = case.context(variant=a.variant, partition=part)
+    ctx = case.context(variant=a.variant, partition=part, debug=True)  # HRT_OPT_GRID_CUS, priority 2
     pc = case.push(1)
     ctx.set_option(_lib.OPT_SPLIT, a.split)
     ctx.set_option(_lib.OPT_PRIORITY, a.prio)
