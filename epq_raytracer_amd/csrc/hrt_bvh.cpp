@@ -489,7 +489,7 @@ extern "C" int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, co
   counts[6] = b.dir_res;
   if (!built) return 0;
   auto copy = [](auto* dst, uint64_t cap, const auto& v) {
-    if (dst && cap >= v.size()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+    if (dst && cap >= v.size() && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
     return !dst || cap >= v.size();
   };
   const bool ok = copy(nodes, nodes_cap, b.nodes) && copy(prims, prims_cap, b.prims) &&

@@ -174,10 +174,12 @@ extern "C" hrt_status hrt_obj_load(const char* path, hrt_obj** out) {
   FILE* f = std::fopen(path, "rb");
   if (!f) return HRT_ERR_IO;
   auto* obj = new hrt_obj();
-  char line[4096];
+  // whole lines of any length (getline grows the buffer): a long 'f' n-gon or 'o' name is never split
+  char* buf = nullptr;
+  size_t cap = 0;
   bool ok = true;
-  while (ok && std::fgets(line, sizeof line, f)) {
-    const char* p = line;
+  while (ok && getline(&buf, &cap, f) != -1) {
+    const char* p = buf;
     while (*p == ' ' || *p == '\t') ++p;
     if (p[0] == 'v' && (p[1] == ' ' || p[1] == '\t')) {
       float x, y, z;
@@ -210,6 +212,7 @@ extern "C" hrt_status hrt_obj_load(const char* path, hrt_obj** out) {
       }
     }
   }
+  std::free(buf);
   std::fclose(f);
   if (!ok) {
     delete obj;

@@ -59,6 +59,7 @@ def load(prefer_fma: bool | None = None) -> ctypes.CDLL:
         prefer_fma = os.environ["ORC_VARIANT"] == "fma"
     fma = _cpu_has_fma() if prefer_fma is None else prefer_fma
     path = os.path.join(BUILD, "liborc_fma.so" if fma else "liborc.so")
+    path = os.environ.get("ORC_LIB", path)  # the sanitizer build (tests/test_sanitizers.py)
     if not os.path.exists(path):
         build()
     _lib = _bind(ctypes.CDLL(path))

@@ -34,6 +34,25 @@ def test_every_declared_symbol_is_exported():
 def test_library_loads_and_reports_abi():
     lib = _lib.load()
     assert lib.hrt_abi_version() == 1
+    assert lib.hrt_debug_build() == 0
+    assert len(_lib.build_id()) == 16 and _lib.build_id() != "unknown"
+
+
+def test_debug_library_is_the_same_abi():
+    """libhip_raytrace_debug.so: the same exports, hrt_debug_build() == 1, the same device code."""
+    dbg = _lib.load(debug=True)
+    assert dbg.hrt_debug_build() == 1 and dbg.hrt_abi_version() == 1
+    assert dbg.hrt_build_id().decode() == _lib.build_id()
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.DEBUG_LIB_PATH], capture_output=True, text=True,
+                         check=True)
+    exported = {line.split()[-1] for line in out.stdout.splitlines() if " T " in line}
+    assert _declared_functions() <= exported
+
+
+def test_rccl_is_not_a_load_time_dependency():
+    """RCCL is dlopen'ed by the first hrt_comm_* call (single-GPU users never load it)."""
+    out = subprocess.run(["readelf", "-d", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    assert "rccl" not in out.stdout
 
 
 def test_code_object_targets_gfx950():

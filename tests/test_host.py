@@ -156,6 +156,23 @@ def test_obj_loader_polygons_negative_indices_and_errors(tmp_path):
         E.load_obj(str(tmp_path / "missing.obj"))
 
 
+def test_obj_loader_long_lines(tmp_path):
+    """lines longer than any fixed buffer (a 3,000-gon face, a 6,000-character object name)
+    are read whole, not split into a parsed head and a silently dropped tail."""
+    n = 3000
+    ang = np.linspace(0, 2 * np.pi, n, endpoint=False)
+    name = "o" * 6000
+    lines = [f"o {name}"] + [f"v {np.cos(a):.6f} {np.sin(a):.6f} 0.25" for a in ang]
+    lines.append("f " + " ".join(f"{i}/{i}/{i}" for i in range(1, n + 1)))
+    p = tmp_path / "long.obj"
+    p.write_text("\n".join(lines) + "\n")
+    assert max(len(line) for line in lines) > 16384
+    ms = E.load_obj(str(p))
+    assert len(ms) == 1 and ms[0].name == name
+    assert len(ms[0].indices) == 3 * (n - 2)
+    assert list(ms[0].indices[-3:]) == [0, n - 2, n - 1]
+
+
 def _rust_f32(s: str) -> np.float32:
     """Correctly rounded decimal -> binary32 (what rustc does for an f32 literal)."""
     q = Fraction(s)
