@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = the library's RCCL gather over xGMI (default); gloo = torch all-gather of the "
                          "local blocks through the host (rehearsal with several ranks on one GPU)")
-    ap.add_argument("--realtime-frames", type=int, default=16,
+    ap.add_argument("--realtime-frames", type=int, default=32,
                     help="after the timed steps: frames of the per-frame dispatch loop (compute_then_render) "
                          "reported as per_frame_dispatch_ms (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length (0 = skip)")
@@ -165,6 +165,7 @@ def main():
     if args.realtime_frames > 0 and fpl > 1:
         saved = fpl
         fpl = 1
+        steps(6)  # untimed: every trace lane's first (probe-planned) trace
         if dist_on:
             dist.barrier()
         ctx.synchronize()
@@ -177,7 +178,7 @@ def main():
         fpl = saved
     kern_ms = st.total_trace_ms / max(st.traces, 1)  # per frame (a launch of f frames counts f traces)
     launches = -(-args.steps // fpl) if fpl > 1 else args.steps
-    last_frame = frame - 1 - (args.realtime_frames if rt_ms is not None else 0)
+    last_frame = frame - 1 - (args.realtime_frames + 6 if rt_ms is not None else 0)
     kernel_sym = _lib.kernel_symbol(st.last_kernel, st.last_block)  # what HRT_KERNEL_AUTO resolved to
     if dist_on:
         t = torch.tensor([elapsed, kern_ms, rt_ms or 0.0], dtype=torch.float64, device=coll_dev)
@@ -214,8 +215,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: reference scene preset (island.obj geometry + src/main.rs materials/camera), "
-                    "deterministic RNG seeds rng_offset = frame index",
+            "data": (f"synthetic: reference scene preset ({args.scene} geometry + src/main.rs materials/camera"
+                     + (", build-defined for cave" if args.scene == "cave" else "") +
+                     "), deterministic RNG seeds rng_offset = frame index"),
             "config": {"workload": f"{args.scene}.obj {W}x{H} {args.spp}spp {args.bounces}-bounce, 1 frame/step "
                                    + (f"(trace + accumulate; the {args.steps} steps as compute_n_then_render: "
                                       f"{launches} trace launch(es) of <= {fpl} frames"

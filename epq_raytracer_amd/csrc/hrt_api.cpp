@@ -649,9 +649,10 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stre
   return HRT_OK;
 }
 
-// The lane the next trace runs on (alternating with HRT_OPT_OVERLAP, after the lane's last reader).
+// The lane the next trace runs on (rotating over HRT_OPT_OVERLAP lanes, after the lane's last reader).
 hrt_status begin_lane(hrt_context* ctx, int* out) {
-  const int l = ctx->overlap && !ctx->diag_on && ctx->lane_used ? ctx->cur_lane ^ 1 : 0;
+  const int n = ctx->diag_on ? 1 : (int)std::max(1u, ctx->overlap);
+  const int l = ctx->lane_used ? (ctx->cur_lane + 1) % n : 0;
   hrt::Lane& lane = ctx->lane[l];
   if (lane.free_set) HRT_HIP(ctx, hipStreamWaitEvent(lane.stream, lane.free, 0));
   *out = l;
@@ -680,6 +681,15 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
     HRT_HIP(ctx, hrt::launch_clear(lane.trace8, lane.trace32, ctx->npix(), lane.stream));
   } else {
     hrt::TraceParams p = make_params(ctx, pc, l);
+    // Throughput mode: when another lane's trace is still running, this one shares the chip with it
+    // (a persistent grid over 1 / HRT_OPT_BUSY_SPLIT of the CUs), so two frames' long sample chains run
+    // side by side instead of the next frame waiting for every CU; an idle GPU gets the whole grid.
+    if (ctx->busy_split > 1) {
+      bool busy = false;
+      for (int o = 0; o < hrt::kLanes; ++o)
+        if (o != l && ctx->lane[o].done_set && hipEventQuery(ctx->lane[o].done) == hipErrorNotReady) busy = true;
+      if (busy) p.num_cus = std::max(1u, p.num_cus / ctx->busy_split);
+    }
     if ((st = launch_frames(ctx, p, lane.stream, l)) != HRT_OK) return st;
   }
   return end_lane(ctx, l);
@@ -1033,8 +1043,13 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       ctx->frames_per_launch = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_OVERLAP:
-      if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "overlap must be 0 or 1");
+      if (value < 0 || value > hrt::kLanes)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "overlap must be 0..3 trace lanes (0 and 1: one lane)");
       ctx->overlap = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_BUSY_SPLIT:
+      if (value < 1 || value > 8) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "busy split must be in [1, 8]");
+      ctx->busy_split = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_WQ_NODE_CAP:
       if (value != 0 && (value < 128 || value > (1 << 20)))

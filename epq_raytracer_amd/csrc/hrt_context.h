@@ -6,11 +6,13 @@
 // the RCCL communicator of the framebuffer gather.
 //
 // Streams.  `stream` (the context's stream, hrt_stream) carries every operation except the trace
-// kernels of hrt_trace, which alternate between two trace lanes, each with its own stream, trace
+// kernels of hrt_trace, which rotate over up to three trace lanes, each with its own stream, trace
 // image, planner buffers and camera lists.  Frame k+1's trace does not depend on frame k's (only the
-// combiner folds them, in order), so with two lanes the next frame's trace starts on the CUs the
-// current one's last work items leave idle (the reference's realtime loop, src/main.rs:41-57,
-// dispatches one trace + combine per frame).  Ordering is by events only:
+// combiner folds them, in order), so the next frame's trace starts on the CUs the current one's last
+// work items leave idle (the reference's realtime loop, src/main.rs:41-57, dispatches one trace +
+// combine per frame).  With three lanes frame k+2's trace waits only for frame k-1's combiner, which
+// has long run, so a combiner that cannot get a CU while a persistent trace holds them all never
+// stalls the next trace.  Ordering is by events only:
 //   * a lane's trace waits for `lane.free` -- recorded on `stream` after the last operation that read
 //     the lane's buffers (the combiner of the frame it traced before, a read_image, compute_n);
 //   * an operation on `stream` that reads a lane's trace image waits for `lane.done`.
@@ -29,7 +31,7 @@
 namespace hrt {
 
 constexpr int kNumCounters = 3 + HRT_NUM_DIAG;  // segments, triangle tests, wave steps, diagnostics
-constexpr int kLanes = 2;
+constexpr int kLanes = 3;  // trace lanes (HRT_OPT_OVERLAP uses 1..kLanes of them)
 
 struct EventPair {
   hipEvent_t start = nullptr, stop = nullptr;
@@ -103,7 +105,8 @@ struct hrt_context {
   hrt::Lane lane[hrt::kLanes];
   int cur_lane = 0;           // lane of the most recent trace (its image is "the trace image")
   bool lane_used = false;     // a trace / init has run since creation
-  uint32_t overlap = 1;       // HRT_OPT_OVERLAP: alternate the lanes (0: every trace on lane 0)
+  uint32_t busy_split = 2;    // HRT_OPT_BUSY_SPLIT: grid share of a trace launched while another runs
+  uint32_t overlap = hrt::kLanes;  // HRT_OPT_OVERLAP: trace lanes in rotation (1: every trace on lane 0)
 
   uint32_t* accum8 = nullptr;
   float4* accum32 = nullptr;

@@ -25,7 +25,7 @@
  * arrays are borrowed for the duration of the call only.  A context is NOT thread-safe: use it from
  * one host thread.  All work on a context is ordered on the context's own HIP stream
  * (== the reference's GpuFuture chaining); hrt_trace / hrt_accumulate return without waiting.
- * Internally a trace runs on one of two trace lanes (own stream + trace image) so that frame k+1's
+ * Internally a trace runs on one of three trace lanes (own stream + trace image) so that frame k+1's
  * trace overlaps frame k's tail; the combiner, reads and every other call stay in call order on the
  * context's stream, so results equal the serial loop's byte for byte (HRT_OPT_OVERLAP).
  */
@@ -221,10 +221,15 @@ typedef enum hrt_option {
   /* hrt_compute_n: frames traced by one persistent launch (default 64, 1 = one launch per frame;
    * also capped at 1 GiB of frame images).  Results do not depend on it. */
   HRT_OPT_FRAMES_PER_LAUNCH = 12,
-  /* hrt_trace: consecutive traces alternate between two trace lanes so that the next frame's trace
-   * starts while the current one finishes (1 default; 0 = one lane, each trace after the previous
-   * frame's combiner).  Results do not depend on it.  Diagnostics (HRT_OPT_COUNTERS = 2) use one lane. */
+  /* hrt_trace: consecutive traces rotate over this many trace lanes (own stream + trace image) so that
+   * the next frame's trace starts while the current one finishes (default 3; 0 or 1 = one lane, each
+   * trace after the previous frame's combiner).  Results do not depend on it.  Diagnostics
+   * (HRT_OPT_COUNTERS = 2) use one lane. */
   HRT_OPT_OVERLAP = 13,
+  /* hrt_trace: a trace issued while another lane's trace still runs launches its persistent grid over
+   * 1/value of the CUs (default 2; 1 = always every CU), so consecutive frames share the chip; a trace
+   * issued to an idle GPU always gets every CU.  Results do not depend on it. */
+  HRT_OPT_BUSY_SPLIT = 14,
   /* libhip_raytrace_debug.so only (tests): the value-th device allocation of the next hrt_set_scene
    * fails with HRT_ERR_OUT_OF_MEMORY (0 = off) */
   HRT_DEBUG_OPT_FAIL_ALLOC = 1001

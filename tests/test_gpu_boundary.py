@@ -18,11 +18,12 @@ from epq_raytracer_amd import rowtiles
 pytestmark = pytest.mark.gpu
 
 
-def _loop(case, frames, first=1, overlap=1, variant=0, mode=_lib.MODE_RGBA8, read_each=False, partition=None,
-          debug=False):
+def _loop(case, frames, first=1, overlap=3, variant=0, mode=_lib.MODE_RGBA8, read_each=False, partition=None,
+          debug=False, busy_split=2):
     ctx = E.HrtContext(case.size, device=0, mode=mode, partition=partition, debug=debug)
     ctx.set_option(_lib.OPT_KERNEL_VARIANT, variant)
     ctx.set_option(_lib.OPT_OVERLAP, overlap)
+    ctx.set_option(_lib.OPT_BUSY_SPLIT, busy_split)
     ctx.set_scene(case.rays, case.spheres, case.tris, case.meshes)
     fmt = _lib.FMT_RGBA8 if mode == _lib.MODE_RGBA8 else _lib.FMT_RGBA32F
     traces = []
@@ -41,6 +42,7 @@ def _loop(case, frames, first=1, overlap=1, variant=0, mode=_lib.MODE_RGBA8, rea
     ("island", (256, 256), 1, 0, _lib.MODE_RGBA8),      # probe-planned first trace on each lane
     ("cave", (64, 48), 2, 7, _lib.MODE_RGBA32F),
     ("box", (45, 33), 3, 5, _lib.MODE_RGBA8),           # non-persistent kernel on the lanes
+    ("island", (640, 360), 8, 0, _lib.MODE_RGBA8),      # traces long enough to overlap (busy split)
 ])
 def test_overlapped_realtime_loop_is_byte_exact(scene, size, spp, variant, mode):
     """compute_then_render per frame (src/raytracing_app.rs:156-194) with the traces alternating
@@ -48,8 +50,8 @@ def test_overlapped_realtime_loop_is_byte_exact(scene, size, spp, variant, mode)
     case = SceneCase(scene, size, spp, 8)
     n = 6
     results = []
-    for overlap in (1, 0):
-        ctx, r = _loop(case, n, first=2, overlap=overlap, variant=variant, mode=mode)
+    for overlap, busy in ((3, 2), (3, 1), (2, 3), (1, 2)):
+        ctx, r = _loop(case, n, first=2, overlap=overlap, variant=variant, mode=mode, busy_split=busy)
         ctx.close()
         results.append(r)
     ctx = case.context(mode=mode, variant=variant)
@@ -67,7 +69,7 @@ def test_overlapped_realtime_loop_is_byte_exact(scene, size, spp, variant, mode)
 def test_overlapped_traces_read_back_in_order():
     """Every trace image read between overlapped traces is that frame's oracle frame."""
     case = SceneCase("island", (80, 48), 2, 8)
-    ctx, (_, _, _, traces) = _loop(case, 4, first=1, overlap=1, read_each=True)
+    ctx, (_, _, _, traces) = _loop(case, 5, first=1, overlap=3, read_each=True)
     ctx.close()
     for k, img in enumerate(traces, start=1):
         ref = case.oracle(rng_offset=k)[0]
@@ -77,7 +79,7 @@ def test_overlapped_traces_read_back_in_order():
 def test_overlap_then_compute_n_then_overlap():
     """Lanes and hrt_compute_n interleaved on one context: the accumulator equals one serial loop."""
     case = SceneCase("island", (96, 64), 2, 8)
-    ref_ctx, (want, want_trace, _, _) = _loop(case, 9, first=1, overlap=0)
+    ref_ctx, (want, want_trace, _, _) = _loop(case, 9, first=1, overlap=1)
     ref_ctx.close()
     ctx = case.context()
     for k in (1, 2):
@@ -253,9 +255,14 @@ def test_production_library_rejects_debug_options():
     ctx.set_option(_lib.OPT_PRIORITY, 0)
     with pytest.raises(_lib.HrtError, match="INVALID"):
         ctx.check_guards()
-    for bad in (-1, 2):
+    for bad in (-1, 4):
         with pytest.raises(_lib.HrtError, match="INVALID"):
             ctx.set_option(_lib.OPT_OVERLAP, bad)
+    for ok in (0, 1, 2, 3):
+        ctx.set_option(_lib.OPT_OVERLAP, ok)
+    for bad in (0, 9):
+        with pytest.raises(_lib.HrtError, match="INVALID"):
+            ctx.set_option(_lib.OPT_BUSY_SPLIT, bad)
     ctx.close()
     dbg = E.HrtContext((16, 16), device=0, debug=True)
     dbg.set_option(_lib.OPT_PRIORITY, 2)
