@@ -948,6 +948,21 @@ extern "C" hrt_status hrt_debug_export_memory(int device, uint64_t bytes, int* f
   return HRT_OK;
 }
 
+// Test support: hrt_math.h's shared-reciprocal normalize / division and sqrt paths against the
+// compiler's IEEE sequences on n hashed inputs; out = {normalize, div3, sqrt mismatches, fast cases}.
+extern "C" hrt_status hrt_debug_math_check(int device, uint32_t n, uint32_t seed, uint64_t out[4]) {
+  if (!out) return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_debug_math_check: null out");
+  unsigned long long* d = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc((void**)&d, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(d, 0, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hrt::launch_math_check(n, seed, d, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(out, d, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  if (d) (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "hrt_debug_math_check");
+  return HRT_OK;
+}
+
 extern "C" hrt_status hrt_debug_unmap_memory(void* ptr, uint64_t size) {
   if (hipMemUnmap(ptr, size) != hipSuccess || hipMemAddressFree(ptr, size) != hipSuccess) return HRT_ERR_HIP;
   return HRT_OK;

@@ -83,6 +83,8 @@ hipError_t launch_accumulate(uint32_t* cur8, const uint32_t* new8, float4* cur32
 // row_words 4-byte words; global row y comes from part (y / row_tile) % parts (hip_raytrace.h partition).
 hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint32_t row_words, uint32_t height,
                                 uint32_t local_rows, uint32_t row_tile, uint32_t parts, hipStream_t stream);
+// hrt_debug_math_check: fast division / sqrt paths vs the IEEE sequences (out[4] device counters).
+hipError_t launch_math_check(uint32_t n, uint32_t seed, unsigned long long* out, hipStream_t stream);
 hipError_t launch_convert(const uint32_t* src8, float4* dst32, const float4* src32, uint32_t* dst8, size_t npix,
                           hipStream_t stream);
 

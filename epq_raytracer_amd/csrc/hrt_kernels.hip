@@ -208,7 +208,7 @@ __device__ __forceinline__ bool shade_step(const Scene& sc, const hrt_push_const
     p.colour = p.colour * ld3(m.colour);
     const float prob = gmax(p.colour.x, gmax(p.colour.y, p.colour.z));
     if (u01(hash(state)) >= prob) return true;
-    p.colour = p.colour / prob;
+    p.colour = div3(p.colour, prob);
     return false;
   }
   p.light = p.light + environment_light(pc, p.dir);
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void trace_literal(TraceParams P) {
       }
       colour = colour + p.light * p.colour;
     }
-    colour = colour / (float)pc.num_samples;
+    colour = div3(colour, (float)pc.num_samples);
     store_pixel(P, x, lr, colour);
   }
   flush_counters(P, segs, tests);
@@ -440,7 +440,7 @@ __device__ __forceinline__ void trace_fused(const TraceParams& P, const Src& src
         p.bounce = pc.max_bounces + 1;
       }
     }
-    colour = colour / (float)pc.num_samples;
+    colour = div3(colour, (float)pc.num_samples);
     store_pixel(P, x, lr, colour);
   }
   flush_counters(P, segs, tests);
@@ -1137,7 +1137,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
     bvh.node(0, R0, R1, R2, R3);
     const float fx = fmaxf(fabsf(o.x - R0.x), fabsf(R1.x - o.x)), fy = fmaxf(fabsf(o.y - R0.y), fabsf(R1.y - o.y));
     const float fz = fmaxf(fabsf(o.z - R0.z), fabsf(R1.z - o.z));
-    R = __builtin_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0001f;
+    R = __builtin_amdgcn_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0001f;  // 1 ulp, inside the x1.0001
   }
   const float abs_t = P.bvh_abs_coef * R;
   const uint32_t end = P.bvh_n_nodes;
@@ -1353,7 +1353,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const float4 R0 = wq.nodes[0], R1 = wq.nodes[1];
     const float fx = fmaxf(fabsf(o.x - R0.x), fabsf(R1.x - o.x)), fy = fmaxf(fabsf(o.y - R0.y), fabsf(R1.y - o.y));
     const float fz = fmaxf(fabsf(o.z - R0.z), fabsf(R1.z - o.z));
-    R = __builtin_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0001f;
+    R = __builtin_amdgcn_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0001f;  // 1 ulp, inside the x1.0001
   }
   const float abs_t = P.bvh_abs_coef * R;
   uint32_t band_tests = 0;
@@ -1414,6 +1414,8 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     ++steps;
     // Step composition (wave-uniform): triangle pairs when >= 64 wait or no node pair is left; when
     // both stacks are short, one mixed step takes them all (lanes [0, nn) node pairs, then triangles).
+    // (Measured, r02: filling a short node step's idle lanes with triangle pairs, or running triangle
+    // steps from 32 waiting pairs, was no faster: 3.699 / 3.722 vs 3.692 ms, profiles/r02g_ab.txt.)
     const bool tri_step = tc >= 64u || nc == 0u;
     const bool mixed = HRT_WQ_MIXED && !tri_step && tc > 0u && nc + tc <= 64u;
     const uint32_t tn = tri_step ? min(64u, tc) : (mixed ? tc : 0u);
@@ -1708,7 +1710,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   }
   if (co.w != 0) return;  // cooperative tile: wave 0 of the group writes the results
   if (active) {
-    colour = colour / (float)pc.num_samples;
+    colour = div3(colour, (float)pc.num_samples);
     store_pixel(P, x, lr, colour, frame);
   }
   if (co.defer) {
@@ -2202,6 +2204,40 @@ __global__ __launch_bounds__(256) void assemble_rows(const uint32_t* __restrict_
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < row_words; i += gridDim.x * 256) dst[i] = src[i];
 }
 
+// Self-check of hrt_math.h's shared-reciprocal division and sqrt paths against the compiler's IEEE
+// sequences, bit for bit, on hashed inputs (exponents over the whole range for a third of the
+// threads, the fast-path range for the rest).  out[0..3]: normalize, div3, sqrt mismatches, fast cases.
+__device__ __forceinline__ float math_check_value(uint32_t& st, bool wide) {
+  const uint32_t h = hash(st), g = hash(st);
+  if (wide) return __builtin_bit_cast(float, h);  // any bit pattern: NaN, inf, denormals, zeros
+  const int e = (int)(g % 100u) - 50;             // |v| in [2^-50, 2^50)
+  const float m = __builtin_bit_cast(float, 0x3f800000u | (h & 0x007fffffu));
+  const float v = __builtin_ldexpf(m, e);
+  return (g >> 31) ? -v : v;
+}
+__global__ __launch_bounds__(256) void math_check(uint32_t n, uint32_t seed, unsigned long long* out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  uint32_t st = seed * 2654435761u + i;
+  const bool wide = (i % 3u) == 0u;
+  const f3 a = mk(math_check_value(st, wide), math_check_value(st, wide), math_check_value(st, wide));
+  const f3 x = normalize(a), y = normalize_ieee(a);
+  const bool bad_n = fbits(x.x) != fbits(y.x) || fbits(x.y) != fbits(y.y) || fbits(x.z) != fbits(y.z);
+  const float sv = __builtin_fabsf(math_check_value(st, wide));
+  const f3 p = div3(a, sv);
+  const bool bad_d = sv > 0.0f && (fbits(p.x) != fbits(a.x / sv) || fbits(p.y) != fbits(a.y / sv) ||
+                                   fbits(p.z) != fbits(a.z / sv));
+  const float q = __builtin_fabsf(math_check_value(st, wide));
+  const bool in = q >= 0x1p-96f && q <= 0x1p80f;
+  const bool bad_s = in && fbits(sqrt_core(q)) != fbits(__builtin_sqrtf(q));
+  const float d2 = dot(a, a);
+  const bool fast = d2 >= 0x1p-80f && d2 <= 0x1p78f;
+  if (bad_n) atomicAdd(&out[0], 1ull);
+  if (bad_d) atomicAdd(&out[1], 1ull);
+  if (bad_s) atomicAdd(&out[2], 1ull);
+  if (fast) atomicAdd(&out[3], 1ull);
+}
+
 }  // namespace hrt
 
 // ---- launch wrappers (host) ----------------------------------------------------------------------
@@ -2455,6 +2491,12 @@ hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint3
     return hipErrorInvalidValue;  // some global row would read outside its part's local rows
   const dim3 g(std::min<uint32_t>((row_words + 255) / 256, 64), height, 1);
   assemble_rows<<<g, 256, 0, stream>>>(gathered, frame, row_words, local_rows, row_tile, parts);
+  return hipGetLastError();
+}
+
+hipError_t launch_math_check(uint32_t n, uint32_t seed, unsigned long long* out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  math_check<<<(n + 255) / 256, 256, 0, stream>>>(n, seed, out);
   return hipGetLastError();
 }
 

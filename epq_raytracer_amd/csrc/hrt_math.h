@@ -36,11 +36,65 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
   return {__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
           __builtin_fmaf(a.x, b.y, -(a.y * b.x))};
 }
-// S4: normalize = v / sqrt(dot(v, v)), correctly rounded divides.
-__device__ __forceinline__ f3 normalize(f3 a) {
-  const float l = __builtin_sqrtf(dot(a, a));
-  return a / l;
+// S4 at the instruction level.  hipcc lowers a correctly rounded f32 '/' to
+//   v_div_scale (den), v_div_scale (num), v_rcp, e = fma(-den, y0, 1), y = fma(e, y0, y0),
+//   q = num * y, r = fma(-den, q, num), q1 = fma(r, y, q), r1 = fma(-den, q1, num),
+//   v_div_fmas (= fma(r1, y, q1) when no scaling), v_div_fixup
+// and a correctly rounded sqrt to a 2^32 pre-scale for tiny inputs, v_sqrt, the two neighbours'
+// fma residual tests, the un-scale and a special-value select.  In the range where V_DIV_SCALE_F32
+// scales nothing (|num|, |den| in [2^-80, 2^40], nonzero: no exponent gap >= 96, no denormal den,
+// 1/den or quotient, num exponent > 23) and V_DIV_FIXUP_F32 passes the finite nonzero quotient
+// through, and where the sqrt input needs no pre-scale and is not special (x in [2^-96, 2^80]), the
+// sequences below ARE the compiler's instructions minus those identities -- the same bits -- and the
+// reciprocal of a common denominator is shared by the three components of a vector.
+// tests/test_gpu_boundary.py::test_fast_division_and_sqrt_match_ieee checks them on the device.
+__device__ __forceinline__ float sqrt_core(float x) {  // x in [2^-96, 2^80]
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sd = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) - 1u);
+  const float su = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) + 1u);
+  float r = __builtin_fmaf(-sd, s, x) <= 0.0f ? sd : s;
+  r = __builtin_fmaf(-su, s, x) > 0.0f ? su : r;
+  return r;
 }
+__device__ __forceinline__ float rcp_core(float den) {  // the refined reciprocal of the '/' sequence
+  const float y0 = __builtin_amdgcn_rcpf(den);
+  return __builtin_fmaf(__builtin_fmaf(-den, y0, 1.0f), y0, y0);
+}
+__device__ __forceinline__ float div_core(float num, float den, float y) {
+  const float q = num * y;
+  const float q1 = __builtin_fmaf(__builtin_fmaf(-den, q, num), y, q);
+  return __builtin_fmaf(__builtin_fmaf(-den, q1, num), y, q1);
+}
+// a / s for s > 0, correctly rounded (the shared-reciprocal path when every lane value is in range)
+__device__ __forceinline__ f3 div3(f3 a, float s) {
+#ifdef HRT_IEEE_DIV  // A/B: the compiler's sequences only
+  return {a.x / s, a.y / s, a.z / s};
+#endif
+  const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+  const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+  const float sum = (a.x + a.y) + a.z;  // fmin / fmax skip a NaN component: this does not
+  if (s >= 0x1p-40f && s <= 0x1p40f && m >= 0x1p-80f && mx <= 0x1p40f && sum == sum) {
+    const float y = rcp_core(s);
+    return {div_core(a.x, s, y), div_core(a.y, s, y), div_core(a.z, s, y)};
+  }
+  return {a.x / s, a.y / s, a.z / s};
+}
+// S4: normalize = v / sqrt(dot(v, v)), correctly rounded sqrt and divides.
+__device__ __forceinline__ f3 normalize(f3 a) {
+#ifdef HRT_IEEE_DIV
+  return a / __builtin_sqrtf(dot(a, a));
+#endif
+  const float d2 = dot(a, a);
+  const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+  if (d2 >= 0x1p-80f && d2 <= 0x1p78f && m >= 0x1p-80f) {  // then |a.c| <= sqrt(d2) <= 2^39
+    const float l = sqrt_core(d2);
+    const float y = rcp_core(l);
+    return {div_core(a.x, l, y), div_core(a.y, l, y), div_core(a.z, l, y)};
+  }
+  return a / __builtin_sqrtf(d2);
+}
+// The reference's spelling of both (for the self-check).
+__device__ __forceinline__ f3 normalize_ieee(f3 a) { return a / __builtin_sqrtf(dot(a, a)); }
 // S6: GLSL 4.60 definitions.
 __device__ __forceinline__ float gmin(float x, float y) { return (y < x) ? y : x; }
 __device__ __forceinline__ float gmax(float x, float y) { return (x < y) ? y : x; }

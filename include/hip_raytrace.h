@@ -372,6 +372,10 @@ hrt_status hrt_release_external_memory(hrt_context* ctx, void* dev_ptr);
  * mapping of it (*ptr, *size rounded to the allocation granularity); hrt_debug_unmap_memory frees it. */
 hrt_status hrt_debug_export_memory(int device, uint64_t bytes, int* fd, void** ptr, uint64_t* size);
 hrt_status hrt_debug_unmap_memory(void* ptr, uint64_t size);
+/* Test support: the kernels' shared-reciprocal normalize / division and sqrt paths (hrt_math.h) vs
+ * the compiler's IEEE sequences, bit for bit, on n hashed inputs of device `device`.
+ * out = {normalize mismatches, division mismatches, sqrt mismatches, fast-path cases}. */
+hrt_status hrt_debug_math_check(int device, uint32_t n, uint32_t seed, uint64_t out[4]);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
 /* The context's HIP stream (hipStream_t), for callers that interoperate: work enqueued on it after

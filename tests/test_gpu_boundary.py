@@ -268,3 +268,15 @@ def test_production_library_rejects_debug_options():
     dbg.set_option(_lib.OPT_PRIORITY, 2)
     dbg.set_option(_lib.OPT_GRID_CUS, 4)
     dbg.close()
+
+
+def test_fast_division_and_sqrt_match_ieee():
+    """hrt_math.h's shared-reciprocal normalize / division and the unscaled sqrt are the compiler's
+    IEEE instruction sequences minus identities in their range: bit-identical on 16M hashed inputs
+    (a third with arbitrary bit patterns -- NaN, inf, denormals, zeros -- which take the IEEE path)."""
+    lib = _lib.load()
+    out = np.zeros(4, np.uint64)
+    for seed in (1, 2, 3, 4):
+        _lib.check(lib.hrt_debug_math_check(0, 1 << 22, seed, _lib.ptr(out)), "hrt_debug_math_check")
+        assert out[0] == 0 and out[1] == 0 and out[2] == 0, out
+        assert out[3] > (1 << 21), out  # most of the non-wide inputs took the fast path
