@@ -85,6 +85,7 @@ hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint3
                                 uint32_t local_rows, uint32_t row_tile, uint32_t parts, hipStream_t stream);
 // hrt_debug_math_check: fast division / sqrt paths vs the IEEE sequences (out[4] device counters).
 hipError_t launch_math_check(uint32_t n, uint32_t seed, unsigned long long* out, hipStream_t stream);
+hipError_t launch_math_check_rng(unsigned long long* out, hipStream_t stream);  // all 2^32 RNG states
 hipError_t launch_convert(const uint32_t* src8, float4* dst32, const float4* src32, uint32_t* dst8, size_t npix,
                           hipStream_t stream);
 

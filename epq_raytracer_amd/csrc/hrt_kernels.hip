@@ -52,11 +52,11 @@ __device__ __forceinline__ uint32_t global_row(uint32_t lr, const TraceParams& p
 __device__ __forceinline__ f3 get_ray_dir(const hrt_push_constants& pc, f3 c, uint32_t& state) {
   const float r = (u01(hash(state)) * 2.0f) * 3.14159265358979323846f;
   float sr, cr;
-  spec_sincos(r, sr, cr);
+  spec_sincos_angle(r, sr, cr);  // r in [0, 2pi]
   const float j = pc.jitter_size;
-  const float s2 = __builtin_sqrtf(u01(hash(state)));
+  const float s2 = sqrt_rng(u01(hash(state)));
   const f3 t1 = ((mk(0.0f, 0.0f, 1.0f) * cr) * j) * s2;
-  const float s3 = __builtin_sqrtf(u01(hash(state)));
+  const float s3 = sqrt_rng(u01(hash(state)));
   const f3 t2 = ((mk(0.0f, 1.0f, 0.0f) * sr) * j) * s3;
   const f3 nc = (c + t1) + t2;
   const float* M = pc.cam_alignment_mat;
@@ -2215,6 +2215,26 @@ __device__ __forceinline__ float math_check_value(uint32_t& st, bool wide) {
   const float v = __builtin_ldexpf(m, e);
   return (g >> 31) ? -v : v;
 }
+// Exhaustive over the 2^32 values of a u01 draw (k = base + thread): sqrt_rng against the compiler's
+// sqrt on u01(k) and on -2 log(u01(k)), and spec_sincos_angle against spec_sincos on the two angle
+// forms of raytracing.glsl (u * 2 * pi and 6.2831852 * u).  out[0..2]: mismatches of each.
+__global__ __launch_bounds__(256) void math_check_rng(uint32_t base, unsigned long long* out) {
+  const uint32_t k = base + blockIdx.x * 256u + threadIdx.x;
+  const float u = u01(k);
+  const float l = -2.0f * spec_log(u);
+  const bool bad_sqrt = fbits(sqrt_rng(u)) != fbits(__builtin_sqrtf(u)) ||
+                        fbits(sqrt_rng(l)) != fbits(__builtin_sqrtf(l));
+  float s0, c0, s1, c1, s2, c2, s3, c3;
+  const float r = (u * 2.0f) * 3.14159265358979323846f, th = 6.2831852f * u;
+  spec_sincos(r, s0, c0);
+  spec_sincos_angle(r, s1, c1);
+  spec_sincos(th, s2, c2);
+  spec_sincos_angle(th, s3, c3);
+  const bool bad_sc = fbits(s0) != fbits(s1) || fbits(c0) != fbits(c1) || fbits(s2) != fbits(s3) ||
+                      fbits(c2) != fbits(c3);
+  if (bad_sqrt) atomicAdd(&out[0], 1ull);
+  if (bad_sc) atomicAdd(&out[1], 1ull);
+}
 __global__ __launch_bounds__(256) void math_check(uint32_t n, uint32_t seed, unsigned long long* out) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
@@ -2492,6 +2512,14 @@ hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint3
   const dim3 g(std::min<uint32_t>((row_words + 255) / 256, 64), height, 1);
   assemble_rows<<<g, 256, 0, stream>>>(gathered, frame, row_words, local_rows, row_tile, parts);
   return hipGetLastError();
+}
+
+hipError_t launch_math_check_rng(unsigned long long* out, hipStream_t stream) {
+  for (uint64_t base = 0; base < (1ull << 32); base += (1ull << 28)) {  // 16 launches of 2^28 states
+    math_check_rng<<<(1u << 28) / 256u, 256, 0, stream>>>((uint32_t)base, out);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_math_check(uint32_t n, uint32_t seed, unsigned long long* out, hipStream_t stream) {

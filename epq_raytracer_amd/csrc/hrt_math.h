@@ -183,6 +183,18 @@ __device__ __forceinline__ float spec_cos(float x) {
   spec_sincos(x, s, c);
   return c;
 }
+// The same for x in [0, 7] (the RNG's angles u * 2pi): the NaN / range guard always passes there.
+__device__ __forceinline__ void spec_sincos_angle(float x, float& s, float& c) {
+  int q;
+  const float r = spec_reduce(x, q);
+  const float ps = sin_poly(r), pc = cos_poly(r);
+  switch (q & 3) {
+    case 0: s = ps; c = pc; break;
+    case 1: s = pc; c = -ps; break;
+    case 2: s = -ps; c = -pc; break;
+    default: s = -pc; c = ps; break;
+  }
+}
 
 // ---- RNG: assets/raytracing.glsl:13-40 ------------------------------------------------------
 __device__ __forceinline__ uint32_t hash(uint32_t& state) {  // :13-21
@@ -199,10 +211,17 @@ __device__ __forceinline__ uint32_t hash(uint32_t& state) {  // :13-21
 // scaleToRange01 :23-25 -- float(4294967295.0) == 2^32, so the divide is an exact power-of-two scale.
 __device__ __forceinline__ float u01(uint32_t s) { return (float)s * 2.3283064365386963e-10f; }
 
+// sqrt on the RNG's values: sqrt_core is the correctly rounded sqrt on every u01 value (k * 2^-32, so 0
+// or >= 2^-32) and on every -2 log(u01) (0 .. 44.4, -0 at u = 1, +inf at u = 0): checked exhaustively
+// over all 2^32 states on the device (hrt_debug_math_check_rng).
+__device__ __forceinline__ float sqrt_rng(float x) { return sqrt_core(x); }
+
 __device__ __forceinline__ float normal_dist(uint32_t& state) {  // :28-33
   const float theta = 6.2831852f * u01(hash(state));  // 2 * 3.1415926 folded exactly
-  const float rho = __builtin_sqrtf(-2.0f * spec_log(u01(hash(state))));
-  return rho * spec_cos(theta);
+  const float rho = sqrt_rng(-2.0f * spec_log(u01(hash(state))));
+  float s, c;
+  spec_sincos_angle(theta, s, c);
+  return rho * c;
 }
 __device__ __forceinline__ f3 unit_sphere(uint32_t& state) {  // :35-40
   const float x = normal_dist(state);

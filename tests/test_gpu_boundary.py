@@ -280,3 +280,12 @@ def test_fast_division_and_sqrt_match_ieee():
         _lib.check(lib.hrt_debug_math_check(0, 1 << 22, seed, _lib.ptr(out)), "hrt_debug_math_check")
         assert out[0] == 0 and out[1] == 0 and out[2] == 0, out
         assert out[3] > (1 << 21), out  # most of the non-wide inputs took the fast path
+
+
+def test_rng_domain_shortcuts_exhaustive():
+    """sqrt_rng (the unscaled sqrt) on every u01 value and every -2 log(u01), and the unguarded sin/cos
+    on both angle forms of raytracing.glsl, equal the general routines for all 2^32 RNG states."""
+    lib = _lib.load()
+    out = np.zeros(2, np.uint64)
+    _lib.check(lib.hrt_debug_math_check_rng(0, _lib.ptr(out)), "hrt_debug_math_check_rng")
+    assert out[0] == 0 and out[1] == 0, out
