@@ -74,7 +74,7 @@ IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
 OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP, OPT_WQ_NODE_CAP, OPT_PROBE = 5, 6, 7, 8, 9, 10, 11
-OPT_FRAMES_PER_LAUNCH, OPT_OVERLAP, OPT_BUSY_SPLIT = 12, 13, 14
+OPT_FRAMES_PER_LAUNCH, OPT_OVERLAP, OPT_BUSY_SPLIT, OPT_BVH_WIDTH = 12, 13, 14, 15
 DEBUG_OPT_FAIL_ALLOC = 1001  # libhip_raytrace_debug.so only
 COMM_ID_BYTES = 128
 COMM_NONE, COMM_RCCL, COMM_RCCL_GROUP, COMM_DEVICE_COPY = 0, 1, 2, 3
@@ -172,7 +172,7 @@ def load(debug: bool = False) -> ctypes.CDLL:
         "hrt_debug_math_check_rng": (c_int32, [c_int32, P]),
         "hrt_debug_bvh_build": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, P, c_uint64, P, c_uint64, P,
                                           c_uint64, P, c_uint64, P, c_uint64]),
-        "hrt_debug_bvh_wq_nodes": (c_int64, [P, c_uint32, P, c_uint32, c_uint32, P, c_uint64]),
+        "hrt_debug_bvh_wq_nodes": (c_int64, [P, c_uint32, P, c_uint32, c_uint32, c_uint32, P, c_uint64]),
         "hrt_host_ray_grid": (c_uint32, [c_uint32, c_uint32, c_float, c_float, POINTER(c_float), POINTER(c_float),
                                          POINTER(c_float), POINTER(c_float), POINTER(c_float)]),
         "hrt_set_option": (c_int32, [P, c_uint32, c_int64]),

@@ -445,7 +445,7 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   s.cam_capacity = (uint32_t)cap;
   // bounce-segment hierarchy (BUNDLE_BVH / BUNDLE_WQ)
   hrt::BvhHost bvh;
-  const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, ctx->bvh_leaf, bvh);
+  const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, ctx->bvh_leaf, bvh, ctx->bvh_width);
   if (built) {
     auto up = [&](auto*& dst, const auto& v, const char* what) -> hrt_status {
       return alloc_upload(ctx, alloc, (void**)&dst, v.data(), v.size() * sizeof(v[0]), what);
@@ -471,6 +471,8 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   s.bvh_rel_t = bvh.rel_t;
   s.bvh_dir_res = bvh.dir_res;
   s.bvh_built_leaf = std::max(1u, std::min(ctx->bvh_leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
+  s.bvh_wq_n = bvh.wq_ok ? bvh.wq_n_nodes : 0u;
+  s.bvh_wq_width = bvh.wq_width;
   s.n_spheres = n_spheres;
   s.n_tris = n_tris;
   s.n_meshes = n_meshes;
@@ -570,6 +572,8 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   const bool built = s.bvh_info[HRT_SCENE_BVH_BUILT] != 0;
   p.bvh_nodes = built ? s.bvh_nodes : nullptr;
   p.bvh_wq_nodes = built ? s.bvh_wq_nodes : nullptr;
+  p.bvh_wq_n_nodes = s.bvh_wq_n;
+  p.bvh_wq_width = s.bvh_wq_width;
   p.bvh_prims = s.bvh_prims;
   p.bvh_irregular = s.bvh_irregular;
   p.bvh_band_off = s.bvh_band_off;
@@ -1089,6 +1093,11 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
     case HRT_OPT_COOP:
       if (value != 0 && value != 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "coop must be 0 or 1");
       ctx->coop = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_BVH_WIDTH:
+      if (value < 2 || value > (int64_t)hrt::kWqMaxWidth)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "BVH width must be in [2, 4]");
+      ctx->bvh_width = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_BVH_LEAF_SIZE:
       if (value < 1 || value > hrt::kBvhMaxLeafCount)

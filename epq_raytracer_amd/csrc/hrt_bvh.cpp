@@ -338,50 +338,86 @@ struct Half {
 
 }  // namespace
 
-bool make_wq_nodes(const BvhHost& b, std::vector<float>& out) {
+bool make_wq_nodes(const BvhHost& b, std::vector<float>& out, uint32_t width, uint32_t* n_out, uint32_t* w_out) {
   out.clear();
-  if (b.n_nodes >= 0x10000u) return false;
+  *n_out = 0;
+  *w_out = 2;
+  width = std::max(2u, std::min(width, kWqMaxWidth));
   static const Half h;
-  out.resize((size_t)b.n_nodes * 12);
   if (b.n_nodes == 0) return true;
   auto word = [&](uint32_t k, int j) {
     uint32_t u;
     std::memcpy(&u, &b.nodes[(size_t)k * 16 + j], 4);
     return u;
   };
-  // sibling-adjacent order: root 0, then every inner node's two children at fc, fc + 1
-  std::vector<uint32_t> new_of(b.n_nodes), esc_of(b.n_nodes), first_child(b.n_nodes, 0);
+  auto is_leaf = [&](uint32_t k) { return (word(k, 14) >> 27) != 0; };
+  auto area = [&](uint32_t k) {
+    const float* r = &b.nodes[(size_t)k * 16];
+    const double ex = std::max(0.0, (double)r[4] - r[0]), ey = std::max(0.0, (double)r[5] - r[1]),
+                 ez = std::max(0.0, (double)r[6] - r[2]);
+    return ex * ey + ey * ez + ex * ez;
+  };
+  // Groups: the children of a kept inner node are its binary children, the inner one of largest
+  // surface area replaced by its own two children (in place, order kept) while the group has fewer
+  // than `width` members.  A kept node's record is its binary node's (the same box, margins and cone);
+  // the collapsed intermediate nodes are never tested.  Slots are allocated depth first.
+  std::vector<uint32_t> new_of(b.n_nodes, ~0u), esc_of(b.n_nodes, 0u), info_of(b.n_nodes, 0u), order;
+  order.reserve(b.n_nodes);
   new_of[0] = 0;
-  esc_of[0] = b.n_nodes;  // end of the walk
-  uint32_t next = 1;
-  for (uint32_t k = 0; k < b.n_nodes; ++k) {  // preorder: a parent precedes its children
-    if (word(k, 14) >> 27) continue;           // leaf
-    const uint32_t l = k + 1, r = word(k, 14);
-    first_child[k] = next;
-    new_of[l] = next;
-    new_of[r] = next + 1;
-    esc_of[l] = next + 1;       // the left child's escape is its sibling
-    esc_of[r] = esc_of[k];      // the right child's is its parent's
-    next += 2;
+  esc_of[0] = 0;  // patched to the node count below
+  order.push_back(0);
+  uint32_t next = 1, widest = 2;
+  std::vector<uint32_t> todo{0};
+  while (!todo.empty()) {
+    const uint32_t k = todo.back();
+    todo.pop_back();
+    if (is_leaf(k)) {
+      info_of[k] = word(k, 14);
+      continue;
+    }
+    std::vector<uint32_t> ch{k + 1, word(k, 14)};
+    while (ch.size() < width) {
+      int best = -1;
+      for (size_t j = 0; j < ch.size(); ++j)
+        if (!is_leaf(ch[j]) && (best < 0 || area(ch[j]) > area(ch[(size_t)best]))) best = (int)j;
+      if (best < 0) break;
+      const uint32_t c = ch[(size_t)best];
+      ch[(size_t)best] = c + 1;
+      ch.insert(ch.begin() + best + 1, word(c, 14));
+    }
+    const uint32_t fc = next, cnt = (uint32_t)ch.size();
+    widest = std::max(widest, cnt);
+    next += cnt;
+    info_of[k] = fc | (cnt - 1u) << 16;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      new_of[ch[j]] = fc + j;
+      esc_of[ch[j]] = j + 1 < cnt ? fc + j + 1 : esc_of[k];  // the last child continues after the parent
+      order.push_back(ch[j]);
+    }
+    for (uint32_t j = cnt; j-- > 0;) todo.push_back(ch[j]);  // depth first, left child on top
   }
-  if (next != b.n_nodes) return false;  // not a full binary tree (cannot happen: every inner node has 2 children)
-  for (uint32_t k = 0; k < b.n_nodes; ++k) {
+  if (next >= 0x10000u) return false;  // 16-bit child and escape indices
+  for (uint32_t k : order)
+    if (esc_of[k] == 0u) esc_of[k] = next;  // the root and the right spine: end of the walk
+  out.resize((size_t)next * 12);
+  for (uint32_t k : order) {
     const float* r = &b.nodes[(size_t)k * 16];
     float* w = &out[(size_t)new_of[k] * 12];
     for (int j = 0; j < 8; ++j) w[j] = r[j];
-    const uint32_t info = word(k, 14);
     uint32_t u[4];
     u[0] = h.conv(r[8], 0) | (uint32_t)h.conv(r[9], 0) << 16;
     u[1] = h.conv(r[10], 0) | (uint32_t)h.conv(r[11], -1) << 16;
     u[2] = h.conv(r[12], +1) | esc_of[k] << 16;
-    u[3] = (info >> 27) ? info : first_child[k];
+    u[3] = info_of[k];
     std::memcpy(&w[8], u, 16);
   }
+  *n_out = next;
+  *w_out = widest;
   return true;
 }
 
 bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
-               uint32_t leaf_size, BvhHost& out) {
+               uint32_t leaf_size, BvhHost& out, uint32_t wq_width) {
   out = BvhHost{};
   if (n_meshes > kBvhMaxMeshes) return false;
   uint64_t total = 0;
@@ -466,7 +502,7 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
   const double e = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)kBandTau - out.rho_max - 4e-7);
   out.abs_coef = round_up(2.1 * (4.2 * e + out.rho_max) * inv_tp * (1.0 + 1e-6));
   out.rel_t = round_up((2.1 * (3.2 * e + out.rho_max) * inv_tp + 4 * e) * (1.0 + 1e-6));
-  out.wq_ok = make_wq_nodes(out, out.wq_nodes);
+  out.wq_ok = make_wq_nodes(out, out.wq_nodes, wq_width, &out.wq_n_nodes, &out.wq_width);
   return true;
 }
 
@@ -499,9 +535,10 @@ extern "C" int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, co
 }
 
 extern "C" int64_t hrt_debug_bvh_wq_nodes(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes,
-                                          uint32_t n_meshes, uint32_t leaf_size, float* out, uint64_t cap) {
+                                          uint32_t n_meshes, uint32_t leaf_size, uint32_t width, float* out,
+                                          uint64_t cap) {
   hrt::BvhHost b;
-  if (!hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf_size, b) || !b.wq_ok || b.wq_nodes.empty()) return 0;
+  if (!hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf_size, b, width) || !b.wq_ok || b.wq_nodes.empty()) return 0;
   if (!out || cap < b.wq_nodes.size()) return -1;
   std::memcpy(out, b.wq_nodes.data(), b.wq_nodes.size() * sizeof(float));
   return (int64_t)(b.wq_nodes.size() / 12);

@@ -43,7 +43,9 @@ struct BvhHost {
   double sah_tri_frac = 0.0;        // expected leaf triangle tests of a uniform random ray / entries
   std::vector<uint32_t> band_list;  // 2 words per entry: prim | n^x << 18, n^y | n^z << 16 (kBand*)
   std::vector<float> wq_nodes;      // BUNDLE_WQ's 48 B node image (make_wq_nodes)
-  bool wq_ok = false;               // the image exists (at most 65535 nodes)
+  bool wq_ok = false;               // the image exists (fewer than 65536 nodes)
+  uint32_t wq_n_nodes = 0;          // its nodes (the binary nodes a group collapse keeps)
+  uint32_t wq_width = 2;            // its largest group (children tested per node pop)
   uint32_t n_nodes = 0, n_prims = 0, n_irregular = 0, n_never = 0;  // never = zero normal (dn == 0)
   double rho_max = 0.0;
   float abs_coef = 0.0f, rel_t = 0.0f;  // box-test t-slack: [-abs_coef R, best (1 + rel_t) + abs_coef R]
@@ -70,22 +72,26 @@ constexpr uint32_t kBvhMaxLeafCount = 16;  // leaf count lives in bits 27..31 of
 constexpr uint64_t kBvhMaxEntries = 1u << 18;
 
 // BUNDLE_WQ node image, 12 floats per node (48 B instead of 64, so cave-sized hierarchies leave
-// room for the pair stacks in LDS), in sibling-adjacent order: root 0, the two children of an inner
-// node at fc and fc + 1 (a (ray, node pair) needs no parent record):
-//   [0..2] box lo, [3] margin a, [4..6] box hi, [7] margin b   (as in the full node)
+// room for the pair stacks in LDS).  A wide tree over a subset of the binary nodes: the children of an
+// inner node are a GROUP of 2..width kept nodes stored side by side at fc .. fc + count - 1 (the binary
+// children, the larger-area inner ones replaced by their own children while the group has room), so
+// a (ray, group) stack entry tests the whole group with no parent record.  Root at 0.
+//   [0..2] box lo, [3] margin a, [4..6] box hi, [7] margin b   (the kept binary node's, unchanged)
 //   [8]  bits: cone axis x | axis y << 16   (binary16, nearest: |error| <= 2^-12 per component)
 //   [9]  bits: cone axis z | cos(phi) << 16 (cos rounded down)
-//   [10] bits: sin(phi) (rounded up) | escape << 16 (left child: its sibling; right child: the
-//        parent's escape; root: n_nodes -- a stackless walk continues there after the subtree)
-//   [11] bits: leaf ? first_prim | count << 27 : first child fc
-// The kernel widens its back-face cone test by the axis error, so the image only ever keeps more.
+//   [10] bits: sin(phi) (rounded up) | escape << 16 (the next member of its group; the last member:
+//        its parent's escape; root: the node count -- a stackless walk continues there after the subtree)
+//   [11] bits: leaf ? first_prim | count << 27 : fc | (group count - 1) << 16
+// The kernel widens its back-face cone test by the axis error, so the image only ever keeps more;
+// skipping a collapsed node's own box test only keeps more as well.
 constexpr float kWqAxisErr = 5e-4f;  // >= sqrt(3) 2^-12: bound on |d.axis_16 - d.axis| for |d| = 1
-bool make_wq_nodes(const BvhHost& b, std::vector<float>& out);
+constexpr uint32_t kWqMaxWidth = 4;  // group width of the default image (HRT_OPT_BVH_WIDTH)
+bool make_wq_nodes(const BvhHost& b, std::vector<float>& out, uint32_t width, uint32_t* n_out, uint32_t* w_out);
 
 // Builds the hierarchy over every (mesh, triangle) entry of the scene.  Returns false (and leaves
 // `out` empty) when the scene has more than kBvhMaxMeshes meshes, kBvhMaxEntries entries or 2^26
 // triangles.
 bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
-               uint32_t leaf_size, BvhHost& out);
+               uint32_t leaf_size, BvhHost& out, uint32_t wq_width = kWqMaxWidth);
 
 }  // namespace hrt

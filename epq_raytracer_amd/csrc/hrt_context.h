@@ -60,6 +60,7 @@ struct SceneBufs {
   uint32_t bvh_info[HRT_NUM_SCENE_INFO] = {};  // hrt_get_scene_info
   float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f;
   uint32_t bvh_built_leaf = 4, bvh_dir_res = 64;
+  uint32_t bvh_wq_n = 0, bvh_wq_width = 2;  // BUNDLE_WQ image: nodes, largest group
 };
 void free_scene(hrt_context* ctx, SceneBufs& s, bool keep_rays);
 
@@ -124,6 +125,7 @@ struct hrt_context {
   uint32_t frame_stack_frames = 0;
   uint32_t num_cus = 0;
   uint32_t bvh_leaf = 4;  // HRT_OPT_BVH_LEAF_SIZE for the next hrt_set_scene
+  uint32_t bvh_width = 4;  // HRT_OPT_BVH_WIDTH for the next hrt_set_scene
   int64_t debug_fail_alloc = 0;  // debug build: fail the n-th device allocation of the next hrt_set_scene
 
   int variant = 0;

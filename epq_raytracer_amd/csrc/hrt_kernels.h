@@ -50,6 +50,8 @@ struct TraceParams {
   // BUNDLE_BVH: bounce-segment hierarchy built by hrt_set_scene (hrt_bvh.h records); nullptr = none.
   const float4* bvh_nodes;       // 4 float4 per node, preorder with escape indices
   const float4* bvh_wq_nodes;    // 3 float4 per node: BUNDLE_WQ's image (hrt_bvh.h make_wq_nodes), or nullptr
+  uint32_t bvh_wq_n_nodes;       // its nodes
+  uint32_t bvh_wq_width;         // its largest group (children per node-stack entry)
   const float4* bvh_prims;       // 4 float4 per leaf triangle
   const float4* bvh_irregular;   // 4 float4 per entry outside the analysis (tested for every ray)
   const uint32_t* bvh_band_off;  // 6 bvh_dir_res^2 + 1 offsets: grazing-band prims per direction cell

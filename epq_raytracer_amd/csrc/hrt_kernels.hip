@@ -1202,22 +1202,18 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // trips as its longest lane (123 per batch vs 55 visits per lane on island) and a leaf's triangles
 // serially, and a heavy 8x8 tile spends ~600K clocks per bounce batch either way (profiles/
 // r01k_tile_profiles.jsonl, BUNDLE_CULL_LDS: ~850 survivor triangles x every lane).  Here the work of
-// a bounce batch is a set of (ray, inner node) and (ray, triangle) PAIRS held in two per-wave LIFO
+// a bounce batch is a set of (ray, node group) and (ray, triangle) PAIRS held in two per-wave LIFO
 // stacks in LDS; every step hands 64 pairs of one kind to the 64 lanes, so lanes stay full whatever the
-// rays' directions.  A node pair tests both children of its node for its ray, pushes the inner ones
-// (the farther first, and all of a step's nearer children above all its farther ones, so the next
-// step descends toward the rays' nearest hits) and the leaves' triangles.  The ray of a pair is read
+// rays' directions.  A node pair tests every member of a group (the 2..4 children of a kept node of
+// the wide image, hrt_bvh.h make_wq_nodes) for its ray, pushes the inner ones (sorted: the farther
+// below, and all of a step's nearest children above all its farther ones, so the next step descends
+// toward the rays' nearest hits) and the leaves' triangles.  The ray of a pair is read
 // from its owner lane (ds_bpermute); its closest hit so far is a 64-bit LDS slot (t bits << 32 |
 // (mesh << 26 | triangle) + 1), lowered with ds_min_u64: the minimum over every triangle the
 // reference accepts of (dist, scan position), i.e. raytracing.glsl's strict '<' in scan order (spheres
 // hold key 0 and win ties, as they are scanned first).  A child is dropped only by BUNDLE_BVH's exact
 // node test (wq_node_visit) against the slot's current t, which only ever exceeds the final one.
-// When the node stack could overflow, the popped pairs' subtrees are walked stacklessly instead.
-#ifndef HRT_WQ_DEEP
-// node steps of at most this many pairs test two levels (lanes would idle).  Off: measured 7.6-7.7 ms
-// without vs 8.2-8.3 ms with 32 on island, no gain on one rank of 8 (profiles/r01n_wq_ab.txt)
-#define HRT_WQ_DEEP 0u
-#endif
+// When the node stack could overflow, the popped groups' subtrees are walked stacklessly instead.
 #ifndef HRT_WQ_CONE
 #define HRT_WQ_CONE 1    // the nodes' back-face (normal cone) test
 #endif
@@ -1227,7 +1223,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 struct WqLds {
   const float4* nodes;        // BVH nodes (LDS copy)
   unsigned long long* slot;   // 64 per wave: closest hit so far per ray (owner lane)
-  uint32_t* ns;               // node-pair stack: first node of a sibling pair << 6 | ray
+  uint32_t* ns;               // node-group stack: group word (fc | (count - 1) << 16) << 6 | ray
   uint32_t* ts;               // triangle-pair stack: leaf prim << 6 | ray
   uint32_t ncap;              // node stack capacity (>= 256)
 };
@@ -1244,6 +1240,16 @@ __device__ __forceinline__ uint32_t wq_info(const float4* nodes, uint32_t k) {  
 }
 __device__ __forceinline__ uint32_t wq_escape(const float4* nodes, uint32_t k) {
   return __builtin_bit_cast(uint32_t, nodes[3 * k + 2].z) >> 16;
+}
+// compare-exchange of two pushed-child slots: the smaller key (the farther child) first
+__device__ __forceinline__ void wq_order(float& ka, uint32_t& ea, float& kb, uint32_t& eb) {
+  const bool sw = kb < ka;
+  const float k = sw ? kb : ka;
+  kb = sw ? ka : kb;
+  ka = k;
+  const uint32_t e = sw ? eb : ea;
+  eb = sw ? ea : eb;
+  ea = e;
 }
 
 // bvh_node_visit on the 48 B image: the cone axis carries up to kWqAxisErr of binary16 error in d.axis
@@ -1384,7 +1390,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       }
     }
   }
-  // pair traversal: the root is tested per lane, then (ray, inner node) / (ray, triangle) pairs
+  // pair traversal: the root is tested per lane, then (ray, node group) / (ray, triangle) pairs
   const uint32_t id0 = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
   wq.slot[lane] = ((unsigned long long)__float_as_uint(c.t) << 32) | id0;
   uint32_t rinfo = 0;
@@ -1396,7 +1402,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   }
   const uint32_t rcnt = rvis ? rinfo >> 27 : 0u;
   const unsigned long long rb = __ballot(rvis && rcnt == 0u);
-  if (rvis && rcnt == 0u) wq.ns[lanes_below(rb)] = (rinfo << 6) | lane;  // inner root: its children's pair
+  if (rvis && rcnt == 0u) wq.ns[lanes_below(rb)] = (rinfo << 6) | lane;  // inner root: its children's group
   uint32_t nc = (uint32_t)__popcll(rb), tc = 0;
   {  // leaf root (a scene of at most leaf-size triangles): its triangles
     uint32_t pre = 0, tot = 0;
@@ -1409,6 +1415,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     for (uint32_t j = 0; j < rcnt; ++j) wq.ts[pre + j] = (((rinfo & 0x07FFFFFFu) + j) << 6) | lane;
     tc = tot;
   }
+  const uint32_t width = P.bvh_wq_width;  // the image's largest group
   uint32_t node_pairs = 0, tri_pairs = 0, steps = 0;
   while (nc | tc) {
     ++steps;
@@ -1433,70 +1440,54 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
     if (is_tri) wq_leaf_prim(P, wq, e >> 6, r, rm, ro, rd);
     if (nn == 0u) continue;
-    // node pairs (ray r, sibling pair c, c + 1): test both -- or, when few pairs are left (deep, lanes
-    // idle), skip an inner node's own box and test its two children, two levels per step.  Leaving
-    // a box untested only ever keeps more.  Slots 0..3 hold the nodes tested by this lane.
+    // node pairs (ray r, group fc .. fc + cnt - 1): test every member.  Slot k: member k's push entry
+    // (its info word << 6 | r when a kept inner node, else ~0u), sort key (minus its box entry
+    // distance when pushed, else -inf), and its triangle count when a kept leaf.
     const f3 rinv = shfl3(inv, r);
     const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
-    const bool deep = nn <= HRT_WQ_DEEP;
-    const bool overflow = nc + (deep ? 4u : 2u) * nn > wq.ncap;  // wave-uniform
-    uint32_t sn[4] = {0u, 0u, 0u, 0u}, si[4] = {0u, 0u, 0u, 0u};
-    bool sk[4] = {false, false, false, false};
-    float st[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const bool overflow = nc + width * nn > wq.ncap;  // wave-uniform
+    uint32_t pe[4] = {~0u, ~0u, ~0u, ~0u}, li[4] = {0u, 0u, 0u, 0u};
+    float pk[4] = {-kFltMax, -kFltMax, -kFltMax, -kFltMax};
     if (is_node) {
-      const uint32_t c = e >> 6;
+      const uint32_t g = e >> 6, fc = g & 0xFFFFu, gcnt = (g >> 16) + 1u;
       if (!overflow) {
-        bool sv[4] = {true, true, false, false};
-        sn[0] = c;
-        sn[1] = c + 1u;
-        if (deep) {
-          const uint32_t il = wq_info(wq.nodes, c), ir = wq_info(wq.nodes, c + 1u);
-          sn[2] = c + 1u;
-          sv[2] = true;
-          sv[1] = false;
-          if ((il >> 27) == 0u) {  // inner left node: its children instead
-            sn[0] = il;
-            sn[1] = il + 1u;
-            sv[1] = true;
-          }
-          if ((ir >> 27) == 0u) {
-            sn[2] = ir;
-            sn[3] = ir + 1u;
-            sv[3] = true;
-          }
-        }
         const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
-#ifndef HRT_WQ_NODE_SERIAL
-        if (!deep) {
-          // both children's records read up front (six LDS reads in flight instead of a chain of
-          // dependent reads behind each child's back-face early-out)
-          const float4* na = wq.nodes + 3 * sn[0];
-          const float4* nb = wq.nodes + 3 * sn[1];
-          const float4 A0 = na[0], A1 = na[1], A2 = na[2], B0 = nb[0], B1 = nb[1], B2 = nb[2];
-          si[0] = __builtin_bit_cast(uint32_t, A2.w);
-          si[1] = __builtin_bit_cast(uint32_t, B2.w);
-          sk[0] = wq_node_visit_r(A0, A1, A2, ro, rd, rinv, rR, rabs, t_hi, st[0]);
-          sk[1] = wq_node_visit_r(B0, B1, B2, ro, rd, rinv, rR, rabs, t_hi, st[1]);
-        } else
-#endif
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (sv[k]) {
-            si[k] = wq_info(wq.nodes, sn[k]);
-            sk[k] = wq_node_visit(wq.nodes + 3 * sn[k], ro, rd, rinv, rR, rabs, t_hi, st[k]);
+        auto member = [&](const float4& N0, const float4& N1, const float4& N2, int k) {
+          float tnear;
+          const uint32_t inf = __builtin_bit_cast(uint32_t, N2.w);
+          if (wq_node_visit_r(N0, N1, N2, ro, rd, rinv, rR, rabs, t_hi, tnear)) {
+            if (inf >> 27) {
+              li[k] = inf;
+            } else {
+              pe[k] = (inf << 6) | r;
+              pk[k] = -tnear;
+            }
           }
+        };
+        {  // every group has >= 2 members: both records read up front (six LDS reads in flight)
+          const float4* na = wq.nodes + 3 * fc;
+          const float4 A0 = na[0], A1 = na[1], A2 = na[2], B0 = na[3], B1 = na[4], B2 = na[5];
+          member(A0, A1, A2, 0);
+          member(B0, B1, B2, 1);
         }
-        // two children: the nearer one in slot 1, pushed above every lane's slot-0 entries (popped first)
-        if (!deep && st[0] < st[1]) {
-          const uint32_t tnode = sn[0], tinfo = si[0];
-          const bool tk = sk[0];
-          const float tt = st[0];
-          sn[0] = sn[1]; si[0] = si[1]; sk[0] = sk[1]; st[0] = st[1];
-          sn[1] = tnode; si[1] = tinfo; sk[1] = tk; st[1] = tt;
+        if (gcnt > 2u) {  // members 2 and 3 (a group of 3 reads member 2 twice and keeps one)
+          const float4* na = wq.nodes + 3 * (fc + 2u);
+          const float4* nb = wq.nodes + 3 * (fc + min(3u, gcnt - 1u));
+          const float4 A0 = na[0], A1 = na[1], A2 = na[2], B0 = nb[0], B1 = nb[1], B2 = nb[2];
+          member(A0, A1, A2, 2);
+          if (gcnt > 3u) member(B0, B1, B2, 3);
         }
-      } else {  // finish the pair's two subtrees with a stackless walk (escape links)
-        const uint32_t end = wq_escape(wq.nodes, c + 1u);
-        uint32_t cur = c;
+        // nearest member last (pushed last = popped first); a 2-wide image leaves slots 2, 3 empty
+        wq_order(pk[0], pe[0], pk[1], pe[1]);
+        if (width > 2u) {
+          wq_order(pk[2], pe[2], pk[3], pe[3]);
+          wq_order(pk[0], pe[0], pk[2], pe[2]);
+          wq_order(pk[1], pe[1], pk[3], pe[3]);
+          wq_order(pk[1], pe[1], pk[2], pe[2]);
+        }
+      } else {  // finish the group's subtrees with a stackless walk (escape links)
+        const uint32_t end = wq_escape(wq.nodes, fc + gcnt - 1u);
+        uint32_t cur = fc;
         while (cur != end) {
           const uint32_t inf = wq_info(wq.nodes, cur), cnt = inf >> 27;
           float tnear;
@@ -1506,21 +1497,21 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
             const uint32_t first = inf & 0x07FFFFFFu;
             for (uint32_t k = first; k < first + cnt; ++k) wq_leaf_prim(P, wq, k, r, rm, ro, rd);
           }
-          cur = (v && !cnt) ? inf : wq_escape(wq.nodes, cur);  // inner: its first child
+          cur = (v && !cnt) ? (inf & 0xFFFFu) : wq_escape(wq.nodes, cur);  // inner: its first child
         }
       }
     }
-    // kept inner nodes: slot-major (every lane's slot 0, then slot 1, ...)
-    uint32_t cnt = 0;
+    // kept inner members: slot-major (every lane's slot 0, then slot 1, ...)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const bool inner = sk[k] && (si[k] >> 27) == 0u;
-      const unsigned long long bk = __ballot(inner);
-      if (inner) wq.ns[nc + lanes_below(bk)] = (si[k] << 6) | r;  // the kept node's children pair
+      if (k >= 2 && width <= 2u) break;
+      const bool push = pe[k] != ~0u;
+      const unsigned long long bk = __ballot(push);
+      if (push) wq.ns[nc + lanes_below(bk)] = pe[k];
       nc += (uint32_t)__popcll(bk);
-      cnt += sk[k] ? si[k] >> 27 : 0u;  // kept leaves' triangle counts
     }
     // kept leaves' triangles: exclusive prefix of the per-lane counts (0..16) from bit-plane ballots
+    const uint32_t cnt = (li[0] >> 27) + (li[1] >> 27) + (li[2] >> 27) + (li[3] >> 27);
     uint32_t pre = 0, tot = 0;
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
@@ -1531,7 +1522,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     uint32_t at = tc + pre;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint32_t c = sk[k] ? si[k] >> 27 : 0u, first = si[k] & 0x07FFFFFFu;
+      const uint32_t c = li[k] >> 27, first = li[k] & 0x07FFFFFFu;
       for (uint32_t j = 0; j < c; ++j) wq.ts[at + j] = ((first + j) << 6) | r;
       at += c;
     }
@@ -2027,7 +2018,7 @@ __global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
 // 1024-thread workgroups).  Dynamic LDS: [nodes x 48 B][16 x (64 slots x 8 B, wq_ncap + wq_tcap words)].
 template <bool D>
 __global__ __launch_bounds__(1024) void trace_bundle_wq(TraceParams P) {
-  const uint32_t nn = P.bvh_n_nodes;
+  const uint32_t nn = P.bvh_wq_n_nodes;
   float4* nodes = lds_tris;
   for (uint32_t k = threadIdx.x; k < 3 * nn; k += 1024) nodes[k] = P.bvh_wq_nodes[k];
   char* base = reinterpret_cast<char*>(nodes + 3 * nn) + (size_t)(threadIdx.x >> 6) * (512 + 4 * (P.wq_ncap + P.wq_tcap));
@@ -2286,7 +2277,8 @@ uint32_t lds_block(uint32_t n) {
 // the 160 KiB after the nodes (at most 1024 pairs, at least 128).  Returns the LDS bytes, 0 = no fit.
 size_t wq_lds_bytes(const TraceParams& p, uint32_t* ncap, uint32_t* tcap) {
   if (!p.bvh_nodes || !p.bvh_wq_nodes || p.bvh_max_leaf > 4) return 0;
-  const size_t nodes = (size_t)p.bvh_n_nodes * 48, t = 64u * (1u + 2u * p.bvh_max_leaf);
+  // a node step pushes up to width x (largest leaf) triangle pairs per lane onto < 64 waiting ones
+  const size_t nodes = (size_t)p.bvh_wq_n_nodes * 48, t = 64u * (1u + p.bvh_wq_width * p.bvh_max_leaf);
   if (nodes + 16 * (512 + 4 * (t + 128)) > kMaxLdsScene) return 0;
   const size_t per_wave = (kMaxLdsScene - nodes) / 16;
   const uint32_t n = (uint32_t)std::min<size_t>(1024, ((per_wave - 512 - 4 * t) / 4) & ~(size_t)63);

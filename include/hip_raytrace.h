@@ -230,6 +230,10 @@ typedef enum hrt_option {
    * 1/value of the CUs (default 2; 1 = always every CU), so consecutive frames share the chip; a trace
    * issued to an idle GPU always gets every CU.  Results do not depend on it. */
   HRT_OPT_BUSY_SPLIT = 14,
+  /* BUNDLE_WQ: children tested per node visit in the hierarchy the next hrt_set_scene builds (2 = the
+   * binary tree, 3 or 4 = groups of up to that many collapsed from it; default 4).  Results do not
+   * depend on it. */
+  HRT_OPT_BVH_WIDTH = 15,
   /* libhip_raytrace_debug.so only (tests): the value-th device allocation of the next hrt_set_scene
    * fails with HRT_ERR_OUT_OF_MEMORY (0 = off) */
   HRT_DEBUG_OPT_FAIL_ALLOC = 1001

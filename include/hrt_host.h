@@ -46,10 +46,11 @@ int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, const hrt_mes
                         uint64_t band_off_cap, uint32_t* band_list, uint64_t band_list_cap);
 
 /* Host-only: the 48-byte node image BUNDLE_WQ stages in LDS (12 floats per node, layout in
- * epq_raytracer_amd/csrc/hrt_bvh.h make_wq_nodes) for the hierarchy hrt_set_scene would build.
- * Returns the node count (out filled), 0 (not built / above 65535 nodes), -1 (cap too small). */
+ * epq_raytracer_amd/csrc/hrt_bvh.h make_wq_nodes) for the hierarchy hrt_set_scene would build with
+ * groups of up to `width` children (HRT_OPT_BVH_WIDTH).  Returns the node count (out filled), 0 (not
+ * built / 65536 nodes or more), -1 (cap too small). */
 int64_t hrt_debug_bvh_wq_nodes(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
-                               uint32_t leaf_size, float* out, uint64_t cap);
+                               uint32_t leaf_size, uint32_t width, float* out, uint64_t cap);
 
 /* Column-major mat4 for push_constants.cam_alignment_mat: columns = normalised direction,
  * new_y, new_z (so mat3(M) * (1,0,0) = direction / |direction|), 4th column (0,0,0,1). */

@@ -249,23 +249,30 @@ def test_leaf_sizes(leaf):
     assert counts.max() <= leaf and counts.sum() == len(b["prims"])
 
 
+def wq_image(case, width, leaf=4):
+    lib = _lib.load()
+    cap = 70000 * 12
+    img = np.zeros(cap, np.float32)
+    got = lib.hrt_debug_bvh_wq_nodes(case.tris.ctypes.data, len(case.tris), case.meshes.ctypes.data,
+                                     len(case.meshes), leaf, width, img.ctypes.data, img.size)
+    assert got > 0
+    return img[:got * 12].reshape(got, 12)
+
+
 @pytest.mark.parametrize("scene", ["island", "cave", "box"])
 def test_wq_node_image(scene):
-    """BUNDLE_WQ's 48 B node image (hrt_bvh.h make_wq_nodes) against the full preorder nodes: the same
-    boxes and margins in sibling-adjacent order (an inner node's children at fc, fc + 1), leaf info
-    copied, escapes that continue a stackless walk after each subtree; the binary16 cone only ever
-    widens (cos rounded down, sin up) and the axis is within 2^-12 per component (kernel: 5e-4)."""
+    """BUNDLE_WQ's 48 B node image (hrt_bvh.h make_wq_nodes) with 2-member groups (the binary tree)
+    against the full preorder nodes: the same boxes and margins in sibling-adjacent order (an inner
+    node's children at fc, fc + 1, group word fc | 1 << 16), leaf info copied, escapes that continue a
+    stackless walk after each subtree; the binary16 cone only ever widens (cos rounded down, sin up)
+    and the axis is within 2^-12 per component (kernel: 5e-4)."""
     case = SceneCase(scene, (8, 8), 1, 1)
     b = build(case.tris, case.meshes, 4)
     if b is None:
         return
-    lib = _lib.load()
     nn = len(b["nodes"])
-    img = np.zeros(nn * 12, np.float32)
-    got = lib.hrt_debug_bvh_wq_nodes(case.tris.ctypes.data, len(case.tris), case.meshes.ctypes.data,
-                                     len(case.meshes), 4, img.ctypes.data, img.size)
-    assert got == nn
-    img = img.reshape(nn, 12)
+    img = wq_image(case, 2)
+    assert len(img) == nn
     w = bits(img[:, 8:12])
     N = b["nodes"]
     Nu = N.view(np.uint32)
@@ -277,7 +284,9 @@ def test_wq_node_image(scene):
         info = int(Nu[k, 14])
         if info >> 27:
             continue
-        fc = int(w[new_of[k], 3])
+        g = int(w[new_of[k], 3])
+        assert g >> 16 == 1  # two members
+        fc = g & 0xFFFF
         left, right = k + 1, info
         new_of[left], new_of[right] = fc, fc + 1
         esc_of[left], esc_of[right] = fc + 1, esc_of[k]
@@ -301,5 +310,59 @@ def test_wq_node_image(scene):
     while cur != nn:
         order.append(cur)
         info = int(w[cur, 3])
-        cur = info if not (info >> 27) else int(w[cur, 2] >> 16)
+        cur = (info & 0xFFFF) if not (info >> 27) else int(w[cur, 2] >> 16)
     assert order == new_of.tolist()
+
+
+@pytest.mark.parametrize("width", [3, 4])
+@pytest.mark.parametrize("scene", ["island", "cave", "box"])
+def test_wq_group_image(scene, width):
+    """The grouped image (HRT_OPT_BVH_WIDTH 3, 4): every record is a binary node's record (box, margins,
+    cone words), a group of 2..width members sits side by side with each member's box inside its
+    parent's, every binary leaf appears exactly once, the collapse keeps the group members in the
+    binary tree's left-to-right order, and a stackless walk (escape links) visits every node once,
+    depth first."""
+    case = SceneCase(scene, (8, 8), 1, 1)
+    b = build(case.tris, case.meshes, 4)
+    if b is None:
+        return
+    img = wq_image(case, width)
+    ref2 = wq_image(case, 2)
+    n = len(img)
+    w = bits(img[:, 8:12])
+    # records are binary-node records (compare against the 2-wide image, whose rows are all nodes)
+    rec = lambda im, k: np.concatenate([bits(im[k, 0:10]), bits(im[k, 10:11]) & 0xFFFF]).tobytes()  # minus escape
+    rows2 = {rec(ref2, k) for k in range(len(ref2))}
+    for k in range(n):
+        assert rec(img, k) in rows2
+    leaves = sorted(int(x) for x in w[:, 3] if x >> 27)
+    Nu = b["nodes"].view(np.uint32)
+    assert leaves == sorted(int(x) for x in Nu[:, 14] if x >> 27)
+    widest, seen, stack = 2, {0}, [0]
+    while stack:
+        k = stack.pop()
+        info = int(w[k, 3])
+        if info >> 27:
+            continue
+        fc, cnt = info & 0xFFFF, (info >> 16) + 1
+        assert 2 <= cnt <= width and fc + cnt <= n
+        widest = max(widest, cnt)
+        prims = [int(w[fc + j, 3]) & 0x07FFFFFF for j in range(cnt) if int(w[fc + j, 3]) >> 27]
+        assert prims == sorted(prims)  # members in the binary tree's order (leaf prims are leaf-ordered)
+        for j in range(cnt):
+            c = fc + j
+            assert c not in seen
+            seen.add(c)
+            assert (img[c, 0:3] >= img[k, 0:3]).all() and (img[c, 4:7] <= img[k, 4:7]).all()
+            assert (img[c, [3, 7]] <= img[k, [3, 7]]).all()  # margins grow toward the root
+            assert int(w[c, 2] >> 16) == (c + 1 if j + 1 < cnt else int(w[k, 2] >> 16) if k else n)
+            stack.append(c)
+    assert seen == set(range(n))
+    if width > 2 and len(b["nodes"]) > 7:
+        assert widest == width and n < len(b["nodes"])
+    order, cur = [], 0
+    while cur != n:
+        order.append(cur)
+        info = int(w[cur, 3])
+        cur = (info & 0xFFFF) if not (info >> 27) else int(w[cur, 2] >> 16)
+    assert sorted(order) == list(range(n))

@@ -122,13 +122,15 @@ def test_coop_tiles_bit_exact(scene, factor):
     ctx.close()
 
 
+@pytest.mark.parametrize("width", [2, 3, 4])
 @pytest.mark.parametrize("cap", [0, 128])
 @pytest.mark.parametrize("split", [0, 1, 64])
 @pytest.mark.parametrize("scene", ["island", "cave", "box", "spheres", "ties"])
-def test_wq_pairs_bit_exact(scene, split, cap):
-    """BUNDLE_WQ: bounce rays through the hierarchy as (ray, node) / (ray, triangle) pairs on per-wave
-    LDS stacks, closest hits merged by (t, scan order) with LDS atomics; cap 128 forces the stackless
-    subtree fallback on most node steps.  Unplanned, then planned (split heavy tiles) traces."""
+def test_wq_pairs_bit_exact(scene, split, cap, width):
+    """BUNDLE_WQ: bounce rays through the hierarchy as (ray, node group) / (ray, triangle) pairs on
+    per-wave LDS stacks, closest hits merged by (t, scan order) with LDS atomics; cap 128 forces the
+    stackless subtree fallback on most node steps; groups of 2 (the binary tree), 3 and 4 children
+    (HRT_OPT_BVH_WIDTH).  Unplanned, then planned (split heavy tiles) traces."""
     sizes = {"island": (75, 41, 3), "cave": (64, 48, 2), "box": (45, 33, 3), "spheres": (40, 30, 2)}
     if scene == "ties":
         case = _tie_soup()
@@ -137,7 +139,7 @@ def test_wq_pairs_bit_exact(scene, split, cap):
         case = SceneCase(scene, (w, h), spp, 8)
     ref, _, seg, tt = case.oracle()
     ctx = case.context(variant=9, options={_lib.OPT_SPLIT: split, _lib.OPT_WQ_NODE_CAP: cap,
-                                           _lib.OPT_SPLIT_FACTOR: 0})
+                                           _lib.OPT_SPLIT_FACTOR: 0, _lib.OPT_BVH_WIDTH: width})
     for _ in range(3):
         ctx.reset_stats()
         ctx.trace(case.push())
