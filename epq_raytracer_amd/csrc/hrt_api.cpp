@@ -445,7 +445,8 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   s.cam_capacity = (uint32_t)cap;
   // bounce-segment hierarchy (BUNDLE_BVH / BUNDLE_WQ)
   hrt::BvhHost bvh;
-  const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, ctx->bvh_leaf, bvh, ctx->bvh_width);
+  const uint32_t leaf = ctx->bvh_leaf ? ctx->bvh_leaf : hrt::auto_leaf_size(cap);
+  const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, bvh, ctx->bvh_width);
   if (built) {
     auto up = [&](auto*& dst, const auto& v, const char* what) -> hrt_status {
       return alloc_upload(ctx, alloc, (void**)&dst, v.data(), v.size() * sizeof(v[0]), what);
@@ -470,7 +471,7 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   s.bvh_abs_coef = bvh.abs_coef;
   s.bvh_rel_t = bvh.rel_t;
   s.bvh_dir_res = bvh.dir_res;
-  s.bvh_built_leaf = std::max(1u, std::min(ctx->bvh_leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
+  s.bvh_built_leaf = std::max(1u, std::min(leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
   s.bvh_wq_n = bvh.wq_ok ? bvh.wq_n_nodes : 0u;
   s.bvh_wq_width = bvh.wq_width;
   s.n_spheres = n_spheres;
@@ -1100,8 +1101,8 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       ctx->bvh_width = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_BVH_LEAF_SIZE:
-      if (value < 1 || value > hrt::kBvhMaxLeafCount)
-        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "BVH leaf size must be in [1, 16]");
+      if (value < 0 || value > hrt::kBvhMaxLeafCount)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "BVH leaf size must be 0 (auto) or in [1, 16]");
       ctx->bvh_leaf = (uint32_t)value;
       return HRT_OK;
 #ifdef HRT_DEBUG_OPTIONS

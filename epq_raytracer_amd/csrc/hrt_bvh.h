@@ -65,6 +65,11 @@ constexpr float kBandQErr = 7e-5f;
 constexpr int kDirResMax = 256;
 inline int dir_res_for(uint64_t entries) { return entries <= 8192 ? 256 : entries <= 32768 ? 128 : 64; }
 
+// Leaf size when HRT_OPT_BVH_LEAF_SIZE is 0 (auto): 2 for scenes BUNDLE_WQ takes (grouped nodes test
+// 4 children per visit, so smaller leaves cost few extra steps and save triangle pairs: island 3.42 ->
+// 3.34 ms, profiles/r02j_wq_groups_ab.jsonl), 4 above (fewer nodes for the LDS-resident hierarchy).
+inline uint32_t auto_leaf_size(uint64_t entries) { return entries <= 8192 ? 2u : 4u; }
+
 constexpr uint32_t kBvhMaxMeshes = 64;     // per-lane mesh filter is a 64-bit mask
 constexpr uint32_t kBvhMaxLeafCount = 16;  // leaf count lives in bits 27..31 of node word 14
 // The grazing-band lists hold ~450 entries (16 B) per triangle on the reference's meshes, so the
@@ -85,13 +90,14 @@ constexpr uint64_t kBvhMaxEntries = 1u << 18;
 // The kernel widens its back-face cone test by the axis error, so the image only ever keeps more;
 // skipping a collapsed node's own box test only keeps more as well.
 constexpr float kWqAxisErr = 5e-4f;  // >= sqrt(3) 2^-12: bound on |d.axis_16 - d.axis| for |d| = 1
-constexpr uint32_t kWqMaxWidth = 4;  // group width of the default image (HRT_OPT_BVH_WIDTH)
+constexpr uint32_t kWqMaxWidth = 4;  // widest group an image may have (HRT_OPT_BVH_WIDTH; the kernel's slots)
+constexpr uint32_t kWqDefaultWidth = 4;
 bool make_wq_nodes(const BvhHost& b, std::vector<float>& out, uint32_t width, uint32_t* n_out, uint32_t* w_out);
 
 // Builds the hierarchy over every (mesh, triangle) entry of the scene.  Returns false (and leaves
 // `out` empty) when the scene has more than kBvhMaxMeshes meshes, kBvhMaxEntries entries or 2^26
 // triangles.
 bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
-               uint32_t leaf_size, BvhHost& out, uint32_t wq_width = kWqMaxWidth);
+               uint32_t leaf_size, BvhHost& out, uint32_t wq_width = kWqDefaultWidth);
 
 }  // namespace hrt

@@ -124,8 +124,8 @@ struct hrt_context {
   void* frame_stack = nullptr;      // hrt_compute_n: frame_stack_frames trace images
   uint32_t frame_stack_frames = 0;
   uint32_t num_cus = 0;
-  uint32_t bvh_leaf = 4;  // HRT_OPT_BVH_LEAF_SIZE for the next hrt_set_scene
-  uint32_t bvh_width = 4;  // HRT_OPT_BVH_WIDTH for the next hrt_set_scene
+  uint32_t bvh_leaf = 0;  // HRT_OPT_BVH_LEAF_SIZE for the next hrt_set_scene (0 = auto, hrt_bvh.h)
+  uint32_t bvh_width = 4;  // HRT_OPT_BVH_WIDTH (hrt_bvh.h kWqDefaultWidth) for the next hrt_set_scene
   int64_t debug_fail_alloc = 0;  // debug build: fail the n-th device allocation of the next hrt_set_scene
 
   int variant = 0;

@@ -1220,6 +1220,14 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
 #endif
+// Widest node group the kernel tests per stack entry (hrt_bvh.h kWqMaxWidth).  Measured (r02,
+// profiles/r02j_wq_groups_ab.jsonl): 8 slots ran the 4-wide image 9% slower (registers), and the
+// triangle stack of an 8-wide image does not fit the LDS; fully ordering the 4 slots (5
+// compare-exchanges, HRT_WQ_FULLSORT) instead of only putting the nearest last (3) was 0.9% slower.
+constexpr uint32_t kWqSlots = 4;
+#ifndef HRT_WQ_FULLSORT
+#define HRT_WQ_FULLSORT 0
+#endif
 struct WqLds {
   const float4* nodes;        // BVH nodes (LDS copy)
   unsigned long long* slot;   // 64 per wave: closest hit so far per ray (owner lane)
@@ -1276,6 +1284,46 @@ __device__ __forceinline__ bool wq_node_visit_r(const float4& N0, const float4& 
 __device__ __forceinline__ bool wq_node_visit(const float4* nd, f3 o, f3 d, f3 inv, float R, float abs_t, float t_hi,
                                               float& t_near) {
   return wq_node_visit_r(nd[0], nd[1], nd[2], o, d, inv, R, abs_t, t_hi, t_near);
+}
+// A node step's ray, prepared once for the group's members (wq_member_visit).
+struct WqRay {
+  f3 o, d, inv;
+  f3 oi;       // RN(o * inv) per axis
+  float sig;   // 2^-23 max |o * inv|: covers the rounding of oi in each slab distance
+  float R, abs_t;
+};
+__device__ __forceinline__ WqRay wq_ray(f3 o, f3 d, f3 inv, float R, float abs_t) {
+  WqRay q;
+  q.o = o;
+  q.d = d;
+  q.inv = inv;
+  q.R = R;
+  q.abs_t = abs_t;
+  q.oi = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+  q.sig = fmaxf(fmaxf(fabsf(q.oi.x), fabsf(q.oi.y)), fabsf(q.oi.z)) * 0x1p-23f;
+  return q;
+}
+// wq_node_visit_r for a prepared ray, each slab distance as fma(bound, inv, -o inv): the exact
+// (bound - o) inv plus at most 2^-24 of the result and 2^-24 |o inv| (the rounding of oi), covered by
+// the 1e-6 relative slack and 2 sig on the interval test (one fma instead of a subtract and a
+// multiply per bound: island 3.242 -> 3.228 ms, profiles/r02k_node_test_ab.txt).  inv = +-inf gives
+// NaN -> visit.  (Measured and dropped: d.axis from binary16 d with v_dot2_f32_f16, 3.345 ms.)
+__device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& N1, const float4& N2, const WqRay& q,
+                                                float t_hi, float& t_near) {
+  const uint32_t w8 = __builtin_bit_cast(uint32_t, N2.x), w9 = __builtin_bit_cast(uint32_t, N2.y),
+                 w10 = __builtin_bit_cast(uint32_t, N2.z);
+  const float x = half_lo(w8) * q.d.x + half_hi(w8) * q.d.y + half_lo(w9) * q.d.z;
+  const float xa = fmaxf(fabsf(x) - (2e-6f + kWqAxisErr), 0.0f);
+  const float s_up = __builtin_amdgcn_sqrtf(fmaxf(1.0f - xa * xa, 0.0f)) + 1.2e-6f;
+  if (HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back
+  const float mg = N0.w + N1.w * q.R;
+  const float tx0 = __builtin_fmaf(N0.x - mg, q.inv.x, -q.oi.x), tx1 = __builtin_fmaf(N1.x + mg, q.inv.x, -q.oi.x);
+  const float ty0 = __builtin_fmaf(N0.y - mg, q.inv.y, -q.oi.y), ty1 = __builtin_fmaf(N1.y + mg, q.inv.y, -q.oi.y);
+  const float tz0 = __builtin_fmaf(N0.z - mg, q.inv.z, -q.oi.z), tz1 = __builtin_fmaf(N1.z + mg, q.inv.z, -q.oi.z);
+  const float tn = fmaxf(fmaxf(-q.abs_t, fminf(tx0, tx1)), fmaxf(fminf(ty0, ty1), fminf(tz0, tz1)));
+  const float tf = fminf(fminf(t_hi, fmaxf(tx0, tx1)), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
+  t_near = tn;
+  return !((tn - fabsf(tn) * 1e-6f) > (tf + fabsf(tf) * 1e-6f) + 2.0f * q.sig);  // NaN -> visit
 }
 
 // Exact reference test (raytracing.glsl:213-241) of BVH leaf prim record (a, -) (e1, -) (e2, -) (n, -):
@@ -1446,8 +1494,15 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const f3 rinv = shfl3(inv, r);
     const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
     const bool overflow = nc + width * nn > wq.ncap;  // wave-uniform
-    uint32_t pe[4] = {~0u, ~0u, ~0u, ~0u}, li[4] = {0u, 0u, 0u, 0u};
-    float pk[4] = {-kFltMax, -kFltMax, -kFltMax, -kFltMax};
+    const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs);
+    uint32_t pe[kWqSlots], li[kWqSlots];
+    float pk[kWqSlots];
+#pragma unroll
+    for (int k = 0; k < (int)kWqSlots; ++k) {
+      pe[k] = ~0u;
+      li[k] = 0u;
+      pk[k] = -kFltMax;
+    }
     if (is_node) {
       const uint32_t g = e >> 6, fc = g & 0xFFFFu, gcnt = (g >> 16) + 1u;
       if (!overflow) {
@@ -1455,7 +1510,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         auto member = [&](const float4& N0, const float4& N1, const float4& N2, int k) {
           float tnear;
           const uint32_t inf = __builtin_bit_cast(uint32_t, N2.w);
-          if (wq_node_visit_r(N0, N1, N2, ro, rd, rinv, rR, rabs, t_hi, tnear)) {
+          if (wq_member_visit(N0, N1, N2, rq, t_hi, tnear)) {
             if (inf >> 27) {
               li[k] = inf;
             } else {
@@ -1464,27 +1519,31 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
             }
           }
         };
-        {  // every group has >= 2 members: both records read up front (six LDS reads in flight)
-          const float4* na = wq.nodes + 3 * fc;
-          const float4 A0 = na[0], A1 = na[1], A2 = na[2], B0 = na[3], B1 = na[4], B2 = na[5];
-          member(A0, A1, A2, 0);
-          member(B0, B1, B2, 1);
+        // members two at a time, both records read up front (six LDS reads in flight); every group
+        // has >= 2 members, and an odd count reads its last member twice and keeps one
+#pragma unroll
+        for (int h = 0; h < (int)kWqSlots / 2; ++h) {
+          if (h == 0 || 2u * h < gcnt) {
+            const float4* na = wq.nodes + 3 * (fc + 2u * h);
+            const float4* nb = wq.nodes + 3 * (fc + min(2u * h + 1u, gcnt - 1u));
+            const float4 A0 = na[0], A1 = na[1], A2 = na[2], B0 = nb[0], B1 = nb[1], B2 = nb[2];
+            member(A0, A1, A2, 2 * h);
+            if (h == 0 || 2u * h + 1u < gcnt) member(B0, B1, B2, 2 * h + 1);
+          }
         }
-        if (gcnt > 2u) {  // members 2 and 3 (a group of 3 reads member 2 twice and keeps one)
-          const float4* na = wq.nodes + 3 * (fc + 2u);
-          const float4* nb = wq.nodes + 3 * (fc + min(3u, gcnt - 1u));
-          const float4 A0 = na[0], A1 = na[1], A2 = na[2], B0 = nb[0], B1 = nb[1], B2 = nb[2];
-          member(A0, A1, A2, 2);
-          if (gcnt > 3u) member(B0, B1, B2, 3);
-        }
-        // nearest member last (pushed last = popped first); a 2-wide image leaves slots 2, 3 empty
+        // the nearest member in the last slot (pushed last = popped first)
+#if HRT_WQ_FULLSORT
         wq_order(pk[0], pe[0], pk[1], pe[1]);
-        if (width > 2u) {
-          wq_order(pk[2], pe[2], pk[3], pe[3]);
-          wq_order(pk[0], pe[0], pk[2], pe[2]);
-          wq_order(pk[1], pe[1], pk[3], pe[3]);
-          wq_order(pk[1], pe[1], pk[2], pe[2]);
-        }
+        wq_order(pk[2], pe[2], pk[3], pe[3]);
+        wq_order(pk[0], pe[0], pk[2], pe[2]);
+        wq_order(pk[1], pe[1], pk[3], pe[3]);
+        wq_order(pk[1], pe[1], pk[2], pe[2]);
+#else
+#pragma unroll
+        for (int st = 1; st < (int)kWqSlots; st *= 2)
+#pragma unroll
+          for (int k = st - 1; k + st < (int)kWqSlots; k += 2 * st) wq_order(pk[k], pe[k], pk[k + st], pe[k + st]);
+#endif
       } else {  // finish the group's subtrees with a stackless walk (escape links)
         const uint32_t end = wq_escape(wq.nodes, fc + gcnt - 1u);
         uint32_t cur = fc;
@@ -1501,17 +1560,19 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         }
       }
     }
-    // kept inner members: slot-major (every lane's slot 0, then slot 1, ...)
+    // kept inner members: slot-major (every lane's slot 0, then slot 1, ...; the ordering may have
+    // moved a member to any slot)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (k >= 2 && width <= 2u) break;
+    for (int k = 0; k < (int)kWqSlots; ++k) {
       const bool push = pe[k] != ~0u;
       const unsigned long long bk = __ballot(push);
       if (push) wq.ns[nc + lanes_below(bk)] = pe[k];
       nc += (uint32_t)__popcll(bk);
     }
     // kept leaves' triangles: exclusive prefix of the per-lane counts (0..16) from bit-plane ballots
-    const uint32_t cnt = (li[0] >> 27) + (li[1] >> 27) + (li[2] >> 27) + (li[3] >> 27);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < (int)kWqSlots; ++k) cnt += li[k] >> 27;
     uint32_t pre = 0, tot = 0;
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
@@ -1521,7 +1582,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     }
     uint32_t at = tc + pre;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < (int)kWqSlots; ++k) {
       const uint32_t c = li[k] >> 27, first = li[k] & 0x07FFFFFFu;
       for (uint32_t j = 0; j < c; ++j) wq.ts[at + j] = ((first + j) << 6) | r;
       at += c;
@@ -2276,7 +2337,7 @@ uint32_t lds_block(uint32_t n) {
 // BUNDLE_WQ per-wave pair stacks: triangle stack 64 x (1 + 2 x largest leaf), node stack what is left of
 // the 160 KiB after the nodes (at most 1024 pairs, at least 128).  Returns the LDS bytes, 0 = no fit.
 size_t wq_lds_bytes(const TraceParams& p, uint32_t* ncap, uint32_t* tcap) {
-  if (!p.bvh_nodes || !p.bvh_wq_nodes || p.bvh_max_leaf > 4) return 0;
+  if (!p.bvh_nodes || !p.bvh_wq_nodes || p.bvh_max_leaf > 4 || p.bvh_wq_width > kWqSlots) return 0;
   // a node step pushes up to width x (largest leaf) triangle pairs per lane onto < 64 waiting ones
   const size_t nodes = (size_t)p.bvh_wq_n_nodes * 48, t = 64u * (1u + p.bvh_wq_width * p.bvh_max_leaf);
   if (nodes + 16 * (512 + 4 * (t + 128)) > kMaxLdsScene) return 0;

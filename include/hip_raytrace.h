@@ -189,7 +189,8 @@ typedef enum hrt_option {
    * or when no lane has a primary segment left (1..64; default 0 = auto: 28 for BUNDLE_WQ, else 48;
    * results do not depend on it) */
   HRT_OPT_SECONDARY_BATCH = 3,
-  /* BUNDLE_BVH: triangles per leaf of the hierarchy the next hrt_set_scene builds (1..16, default 4) */
+  /* BUNDLE_BVH / BUNDLE_WQ: triangles per leaf of the hierarchy the next hrt_set_scene builds (1..16;
+   * default 0 = auto: 2 up to 8192 mesh triangles, else 4) */
   HRT_OPT_BVH_LEAF_SIZE = 4,
   /* persistent kernels: a heavy tile (HRT_OPT_SPLIT_FACTOR) of the previous trace runs as this many
    * work items of 8/k rows each, scheduled first: at most this many (1 = off, 2, 4, 8; default 0 =

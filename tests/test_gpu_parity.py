@@ -65,8 +65,10 @@ def test_split_schedule_bit_exact(scene, size, spp, bounces, variant, split, fac
     Every plan gives the oracle's frame and counts."""
     case = SceneCase(scene, size, spp, bounces)
     ref, _, seg, tt = case.oracle()
+    # BUNDLE_BVH_LDS holds the whole hierarchy in LDS: island's fits with leaves of 4 (not the auto 2)
     ctx = case.context(variant=variant, options={_lib.OPT_SPLIT: split, _lib.OPT_SPLIT_FACTOR: factor,
-                                                 _lib.OPT_PRIORITY: prio})
+                                                 _lib.OPT_PRIORITY: prio,
+                                                 _lib.OPT_BVH_LEAF_SIZE: 4 if variant == 8 else 0})
     for _ in range(3):  # unplanned, planned from an unsplit trace, planned from a split one
         ctx.reset_stats()
         ctx.trace(case.push())
@@ -138,8 +140,9 @@ def test_wq_pairs_bit_exact(scene, split, cap, width):
         w, h, spp = sizes[scene]
         case = SceneCase(scene, (w, h), spp, 8)
     ref, _, seg, tt = case.oracle()
-    ctx = case.context(variant=9, options={_lib.OPT_SPLIT: split, _lib.OPT_WQ_NODE_CAP: cap,
-                                           _lib.OPT_SPLIT_FACTOR: 0, _lib.OPT_BVH_WIDTH: width})
+    # (cave with the auto leaf size 2 does not fit the LDS at width 2: leaves of 4 there)
+    ctx = case.context(variant=9, options={_lib.OPT_SPLIT: split, _lib.OPT_WQ_NODE_CAP: cap, _lib.OPT_SPLIT_FACTOR: 0,
+                                           _lib.OPT_BVH_WIDTH: width, _lib.OPT_BVH_LEAF_SIZE: 4 if scene == "cave" else 0})
     for _ in range(3):
         ctx.reset_stats()
         ctx.trace(case.push())
