@@ -30,6 +30,17 @@
 
 namespace hrt {
 
+#ifdef HRT_EXP_TWICE
+// Timing experiments only (frames unchanged): run one phase a second time on opaque copies of its
+// inputs and discard the result, so the time difference is that phase's marginal cost.
+__device__ __forceinline__ float exp_zero() {
+  float z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
+__device__ __forceinline__ void exp_use(float v) { asm volatile("; use %0" ::"v"(v)); }
+#endif
+
 // Read-only views of the uploaded std430 records.
 struct Scene {
   const float4* __restrict__ rays;
@@ -506,7 +517,8 @@ struct Diag {
   uint32_t bvh_visits = 0, bvh_prims = 0, bvh_band = 0;  // per lane (BUNDLE_BVH)
   uint64_t cyc_prim = 0, cyc_sec = 0, cyc_shade = 0;  // shader clocks per wave and phase
   uint32_t sec_stage2 = 0, sec_front = 0;
-  uint32_t bvh_trips = 0, bvh_leaf_trips = 0;  // BUNDLE_BVH: wave-level traversal trips                // bounce survivors reaching stage 2 / with a front-facing lane
+  uint32_t bvh_trips = 0, bvh_leaf_trips = 0;  // BUNDLE_BVH: wave-level traversal trips
+  uint32_t band_max = 0, band_len = 0;          // BUNDLE_WQ: longest band list per batch / every lane's, summed
 };
 
 __device__ __forceinline__ float wave_min_all(float v) {  // all 64 lanes active
@@ -612,6 +624,7 @@ struct TileList {
   // bit 8m + (sx | sy << 1 | sz << 2) (aabb_truth_table); aabb_ok false -> the literal test
   unsigned long long aabb;
   bool aabb_ok;
+  uint32_t tsum;  // lane l: the triangle tests of a primary ray in octant l & 7 (sum of passing meshes' len)
 };
 
 // intersecting_aabb's result for origin o depends only on the signs of (bound - o) and of 1/d per
@@ -626,6 +639,7 @@ __device__ __forceinline__ void aabb_truth_table(const TraceParams& P, TileList&
   const uint32_t lane = threadIdx.x & 63, m = lane >> 3, oct = lane & 7;
   const f3 o = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
   bool pass = false, bad = false;
+  uint32_t len = 0;
   if (m < (uint32_t)pc.num_meshes) {
     const hrt_mesh& mesh = P.meshes[m];
     for (int a = 0; a < 3; ++a) {
@@ -634,9 +648,15 @@ __device__ __forceinline__ void aabb_truth_table(const TraceParams& P, TileList&
       bad |= !(lo < 0.0f || lo > 0.0f) || !(hi < 0.0f || hi > 0.0f);  // zero or NaN
     }
     pass = aabb_pass(mesh, o, mk((oct & 1) ? -1.0f : 1.0f, (oct & 2) ? -1.0f : 1.0f, (oct & 4) ? -1.0f : 1.0f));
+    len = pass ? mesh.len : 0u;
   }
   t.aabb = __ballot(pass);
   t.aabb_ok = pc.num_meshes <= 8 && !__any(bad);
+  // per octant: the tests counter's increment (lanes oct, oct + 8, ... hold its meshes)
+  len += (uint32_t)__shfl_xor((int)len, 8, 64);
+  len += (uint32_t)__shfl_xor((int)len, 16, 64);
+  len += (uint32_t)__shfl_xor((int)len, 32, 64);
+  t.tsum = len;
 }
 
 __device__ __forceinline__ Bundle tile_bundle(const hrt_push_constants& pc, bool active, f3 centre, bool& ok) {
@@ -676,7 +696,7 @@ __device__ __forceinline__ bool bundle_keep(const float4* __restrict__ cr, uint3
 // Builds the wave's list (all 64 lanes active; the caller synchronises before reading it).
 __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool active, f3 centre, uint32_t* lds) {
   const hrt_push_constants& pc = P.pc;
-  TileList t{0u, lds, 0u, false, 0ull, false};
+  TileList t{0u, lds, 0u, false, 0ull, false, 0u};
   const uint32_t cap = lds ? kTileCapLds : kTileCapVgpr;
   if (pc.num_meshes > 32 || !__any(active)) return t;
   bool ok;
@@ -720,39 +740,62 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
                                                f3 o, f3 d, uint32_t& tests, Closest& c) {
   const hrt_push_constants& pc = P.pc;
   spheres_first(sc, pc, prim, o, d, c);
-  uint32_t pass_mask = 0;
-  // primary lanes start at cam_pos (the table's origin)
+  // primary lanes start at cam_pos (the table's origin): bit 8m of pm is mesh m's AABB test, by the
+  // direction's octant (one 64-bit shift of the wave's table and one lane read of its test count) or,
+  // off the table's domain, by the literal test
   const bool octant = tl.aabb_ok && fabsf(d.x) <= 1.5f && fabsf(d.y) <= 1.5f && fabsf(d.z) <= 1.5f;
+  const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
+  unsigned long long pm = tl.aabb >> oct;
+  const uint32_t oct_tests = (uint32_t)__shfl((int)tl.tsum, (int)oct, 64);
   if (prim && octant) {
-    const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
-    const unsigned long long row = tl.aabb >> oct;
-    for (int m = 0; m < pc.num_meshes; ++m) {
-      if ((row >> (8 * m)) & 1ull) {
-        pass_mask |= 1u << m;
-        tests += sc.meshes[m].len;
-      }
-    }
+    tests += oct_tests;
   } else if (prim) {
+    pm = 0ull;
     for (int m = 0; m < pc.num_meshes; ++m) {
       if (aabb_pass(sc.meshes[m], o, d)) {
-        pass_mask |= 1u << m;
+        pm |= 1ull << (8 * m);
         tests += sc.meshes[m].len;
       }
     }
   }
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 6
+  {
+    const float z = exp_zero();
+    const f3 d2 = mk(d.x + z, d.y + z, d.z + z);
+    const uint32_t o2 = (fbits(d2.x) >> 31) | ((fbits(d2.y) >> 31) << 1) | ((fbits(d2.z) >> 31) << 2);
+    exp_use((float)(uint32_t)(tl.aabb >> o2) + (float)(uint32_t)__shfl((int)tl.tsum, (int)o2, 64));
+  }
+#endif
   float best_k = c.t * kOnePlus;
   const kfloat* ct = to_const(P.cam_tris);
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 7
+  {
+    const float z = exp_zero();
+    const f3 d2 = mk(d.x + z, d.y + z, d.z + z);
+    Closest c2 = c;
+    float bk2 = best_k;
+    for (uint32_t i = 0; i < tl.n; ++i) {
+      const uint32_t e = tl.lds ? __builtin_amdgcn_readfirstlane(tl.lds[i])
+                                : (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
+      const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
+      const bool pass = prim && ((pm >> (8 * m)) & 1ull);
+      if (!__any(pass)) continue;
+      const kf16 R = ld_rec(ct, kk);
+      const float dn = pass ? dot(d2, mk(R[12], R[13], R[14])) : 0.0f;
+      if (__any(dn < 0.0f))
+        primary_exact_rec(make_float4(R[0], R[1], R[2], R[3]), make_float4(R[4], R[5], R[6], R[7]),
+                          make_float4(R[8], R[9], R[10], R[11]), dn, d2, m, c2, bk2);
+    }
+    exp_use(c2.t + (float)c2.idx);
+  }
+#endif
   for (uint32_t i = 0; i < tl.n; ++i) {
     const uint32_t e = tl.lds ? __builtin_amdgcn_readfirstlane(tl.lds[i])
                               : (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
-    const bool pass = (pass_mask >> m) & 1u;
+    const bool pass = prim && ((pm >> (8 * m)) & 1ull);
     if (!__any(pass)) continue;
-#ifdef HRT_PRIM_SPLIT_LOADS
-    const float4 N = ldk(ct, 4 * kk + 3);
-    const float dn = pass ? dot(d, mk(N.x, N.y, N.z)) : 0.0f;
-    if (__any(dn < 0.0f)) primary_exact(ct, kk, dn, d, m, c, best_k);
-#else
+    {
     // the whole record in one load: the exact test's operands arrive with the normal (one K$ round
     // trip per entry instead of two dependent ones)
     const kf16 R = ld_rec(ct, kk);
@@ -760,7 +803,7 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
     if (__any(dn < 0.0f))
       primary_exact_rec(make_float4(R[0], R[1], R[2], R[3]), make_float4(R[4], R[5], R[6], R[7]),
                         make_float4(R[8], R[9], R[10], R[11]), dn, d, m, c, best_k);
-#endif
+    }
   }
 }
 
@@ -1401,6 +1444,21 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   const BvhGlobal g{P.bvh_nodes, P.bvh_prims};
   for (uint32_t k = 0; k < P.bvh_n_irregular; ++k)
     if (sec) bvh_prim_test(P.bvh_irregular, k, mask, o, d, c, bkey, best_k);
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 9
+  {
+    const float z = exp_zero();
+    const f3 d2 = mk(d.x + z, d.y + z, d.z + z);
+    unsigned long long m2 = 0ull;
+    uint32_t t2 = 0;
+    if (sec)
+      for (int m = 0; m < pc.num_meshes; ++m)
+        if (aabb_pass(sc.meshes[m], o, d2)) {
+          m2 |= 1ull << m;
+          t2 += sc.meshes[m].len;
+        }
+    exp_use((float)m2 + (float)t2);
+  }
+#endif
   const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float R;
   {  // farthest root-box corner from the origin, rounded up
@@ -1410,7 +1468,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     R = __builtin_amdgcn_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0001f;  // 1 ulp, inside the x1.0001
   }
   const float abs_t = P.bvh_abs_coef * R;
-  uint32_t band_tests = 0;
+  uint32_t band_tests = 0, band_lmax = 0;
 #ifdef HRT_WQ_NOBAND
   if (false) {
 #else
@@ -1418,6 +1476,10 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #endif
     const uint32_t cell = dir_cell(d, P.bvh_dir_res);
     const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
+    if (D && P.diag) {
+      dg.band_len += b1 - b0;
+      band_lmax = b1 - b0;
+    }
     const BandCheck bc(d, -kBandTau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
     uint32_t k = b0;
     for (; k + 4 <= b1; k += 4) {
@@ -1438,6 +1500,23 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       }
     }
   }
+#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 8
+  if (sec && mask) {
+    const float z = exp_zero();
+    const f3 d2 = mk(d.x + z, d.y + z, d.z + z);
+    Closest c2 = c;
+    uint32_t bk2 = 0;
+    float bbk2 = best_k;
+    const uint32_t cell = dir_cell(d2, P.bvh_dir_res);
+    const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
+    const BandCheck bc(d2, -kBandTau - 2e-5f, 3e-5f);
+    for (uint32_t k = b0; k < b1; ++k) {
+      const uint2 q = P.bvh_band[k];
+      if (bc.in(q)) g.prim(BandCheck::prim(q), mask, o, d2, c2, bk2, bbk2);
+    }
+    exp_use(c2.t + (float)bk2);
+  }
+#endif
   // pair traversal: the root is tested per lane, then (ray, node group) / (ray, triangle) pairs
   const uint32_t id0 = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
   wq.slot[lane] = ((unsigned long long)__float_as_uint(c.t) << 32) | id0;
@@ -1601,6 +1680,8 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       dg.bvh_trips += steps;
     }
     dg.bvh_band += band_tests;
+    const uint32_t bm = wave_max_u(band_lmax);
+    if (lane == 0) dg.band_max += bm;
   }
 }
 
@@ -1609,16 +1690,6 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 // segments take the bundle path; a lane whose next segment is a bounce waits (state untouched) until
 // at least sec_batch lanes wait or no primary segment is left in the wave, then all waiting lanes run
 // their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
-#ifdef HRT_EXP_TWICE
-// Timing experiments only (frames unchanged): run one phase a second time on opaque copies of its
-// inputs and discard the result, so the time difference is that phase's marginal cost.
-__device__ __forceinline__ float exp_zero() {
-  float z;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-  return z;
-}
-__device__ __forceinline__ void exp_use(float v) { asm volatile("; use %0" ::"v"(v)); }
-#endif
 
 enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2, kBounceWq = 3 };
 
@@ -1799,6 +1870,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[14], (unsigned long long)dg.sec_front);
     atomicAdd(&P.diag[15], (unsigned long long)dg.bvh_trips);
     atomicAdd(&P.diag[16], (unsigned long long)dg.bvh_leaf_trips);
+    atomicAdd(&P.diag[17], (unsigned long long)dg.band_max);
     atomicAdd(&P.diag[0], (unsigned long long)dg.prim_iters);
     atomicAdd(&P.diag[1], (unsigned long long)dg.prim_considered);
     atomicAdd(&P.diag[2], (unsigned long long)dg.prim_survivors);
@@ -1811,6 +1883,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[7], (unsigned long long)dg.bvh_visits);
     atomicAdd(&P.diag[8], (unsigned long long)dg.bvh_prims);
     atomicAdd(&P.diag[9], (unsigned long long)dg.bvh_band);
+    atomicAdd(&P.diag[18], (unsigned long long)dg.band_len);
   }
 }
 

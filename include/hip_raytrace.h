@@ -259,7 +259,9 @@ typedef enum hrt_diag {
   HRT_DIAG_BOUNCE_FRONT = 14,      /* ... and some such lane front-facing (dn < 0) */
   HRT_DIAG_BVH_TRIPS = 15,         /* BUNDLE_BVH: traversal loop iterations per bounce batch (wave), summed */
   HRT_DIAG_BVH_LEAF_TRIPS = 16,    /* ... of which some lane tested a leaf */
-  HRT_NUM_DIAG = 17
+  HRT_DIAG_BAND_SCAN_MAX = 17,     /* BUNDLE_WQ: grazing-band entries of the longest list per bounce batch, summed */
+  HRT_DIAG_BAND_SCAN_LEN = 18,     /* ... of every bounce lane's list, summed */
+  HRT_NUM_DIAG = 19
 } hrt_diag;
 
 /* What hrt_set_scene built for BUNDLE_BVH (hrt_get_scene_info). */

@@ -99,6 +99,8 @@ def main():
                 d["bvh_leaf_trips_per_iter"] = d["bvh_leaf_trips"] / max(d["bounce_iters"], 1)
                 d["primary_cycles_per_iter"] = d["primary_cycles"] / max(d["primary_iters"], 1)
                 d["primary_list_len"] = d["primary_considered"] / max(d["primary_iters"], 1)
+                d["band_max_per_batch"] = d.get("band_scan_max", 0) / max(d["bounce_iters"], 1)
+                d["band_len_per_lane"] = d.get("band_scan_len", 0) / max(d["bounce_lanes"], 1)
                 print(json.dumps(d), flush=True)
                 ctx.set_option(_lib.OPT_COUNTERS, 1)
     out = []
