@@ -179,13 +179,43 @@ __device__ __forceinline__ f3 environment_light(const hrt_push_constants& pc, f3
 }
 
 // adjust_dir, raytracing.glsl:297-305 (both unit-sphere draws always happen: 12 hashes)
+#ifndef HRT_FUZZ_FAST
+#define HRT_FUZZ_FAST 1
+#endif
 __device__ __forceinline__ f3 adjust_dir(f3 d, f3 n, const hrt_material& mat, bool specular, uint32_t& state) {
   const f3 diffuse_dir = normalize(n + unit_sphere(state));
   const float k = 2.0f * dot(n, d);
   const f3 specular_dir = d - n * k;
-  const f3 fuzz = unit_sphere(state) * mat.settings[2];
   const float a = mat.settings[1] * (float)(int)specular;
   const float oma = 1.0f - a;
+#if HRT_FUZZ_FAST
+  // Without fuzz and specular blend (settings[2] == +-0, a == +-0: a Lambertian hit), mixed + fuzz is
+  // diffuse_dir * 1 + specular_dir * (+-0) + unit_sphere * (+-0) component by component, i.e.
+  // diffuse_dir itself when each of its components is finite and nonzero (adding a signed zero keeps
+  // it), specular_dir is finite, and the fuzz draw is finite: each of its three normal_dist radii
+  // sqrt(-2 log u) is finite and nonzero exactly when u01 of its second hash is neither 0 nor 1
+  // (spec_log(1) = +0, spec_log(0) = -inf; cos of the angle is never 0, hrt_math.h), so its length
+  // is not 0.  Such a lane only advances the RNG by the draw's six hashes.
+  const float fz = mat.settings[2];
+  uint32_t st = state;
+  bool fast = a == 0.0f && fz == 0.0f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    hash(st);  // the angle's
+    const float u = u01(hash(st));
+    fast &= u != 0.0f && u != 1.0f;
+  }
+  const bool finite_nz = fabsf(diffuse_dir.x) < __builtin_inff() && fabsf(diffuse_dir.y) < __builtin_inff() &&
+                         fabsf(diffuse_dir.z) < __builtin_inff() && diffuse_dir.x != 0.0f && diffuse_dir.y != 0.0f &&
+                         diffuse_dir.z != 0.0f;
+  const bool spec_ok = fabsf(specular_dir.x) < __builtin_inff() && fabsf(specular_dir.y) < __builtin_inff() &&
+                       fabsf(specular_dir.z) < __builtin_inff();
+  if (fast && finite_nz && spec_ok) {
+    state = st;
+    return normalize(diffuse_dir);
+  }
+#endif
+  const f3 fuzz = unit_sphere(state) * mat.settings[2];
   const f3 mixed = mk(diffuse_dir.x * oma + specular_dir.x * a, diffuse_dir.y * oma + specular_dir.y * a,
                       diffuse_dir.z * oma + specular_dir.z * a);
   return normalize(mixed + fuzz);
@@ -2342,7 +2372,9 @@ __device__ __forceinline__ float math_check_value(uint32_t& st, bool wide) {
 }
 // Exhaustive over the 2^32 values of a u01 draw (k = base + thread): sqrt_rng against the compiler's
 // sqrt on u01(k) and on -2 log(u01(k)), and spec_sincos_angle against spec_sincos on the two angle
-// forms of raytracing.glsl (u * 2 * pi and 6.2831852 * u).  out[0..2]: mismatches of each.
+// forms of raytracing.glsl (u * 2 * pi and 6.2831852 * u); and adjust_dir's Lambertian shortcut
+// premise: a normal_dist radius sqrt(-2 log u) is finite and nonzero iff u is neither 0 nor 1, and the
+// cosine of 6.2831852 u is never 0.  out[0..2]: violations of each.
 __global__ __launch_bounds__(256) void math_check_rng(uint32_t base, unsigned long long* out) {
   const uint32_t k = base + blockIdx.x * 256u + threadIdx.x;
   const float u = u01(k);
@@ -2357,8 +2389,12 @@ __global__ __launch_bounds__(256) void math_check_rng(uint32_t base, unsigned lo
   spec_sincos_angle(th, s3, c3);
   const bool bad_sc = fbits(s0) != fbits(s1) || fbits(c0) != fbits(c1) || fbits(s2) != fbits(s3) ||
                       fbits(c2) != fbits(c3);
+  const float rho = sqrt_rng(l);
+  const bool rho_nz = fabsf(rho) < __builtin_inff() && rho != 0.0f;
+  const bool bad_fast = rho_nz != (u != 0.0f && u != 1.0f) || c3 == 0.0f;
   if (bad_sqrt) atomicAdd(&out[0], 1ull);
   if (bad_sc) atomicAdd(&out[1], 1ull);
+  if (bad_fast) atomicAdd(&out[2], 1ull);
 }
 __global__ __launch_bounds__(256) void math_check(uint32_t n, uint32_t seed, unsigned long long* out) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;

@@ -385,8 +385,8 @@ hrt_status hrt_debug_unmap_memory(void* ptr, uint64_t size);
 hrt_status hrt_debug_math_check(int device, uint32_t n, uint32_t seed, uint64_t out[4]);
 /* Test support: the kernels' RNG-domain shortcuts (sqrt of u01 draws and of -2 log(u01), sin/cos of the
  * RNG's angles without the range guard) against the general routines over all 2^32 states.
- * out = {sqrt mismatches, sincos mismatches}. */
-hrt_status hrt_debug_math_check_rng(int device, uint64_t out[2]);
+ * out = {sqrt mismatches, sincos mismatches, Lambertian-shortcut premise violations (hrt_kernels.hip adjust_dir)}. */
+hrt_status hrt_debug_math_check_rng(int device, uint64_t out[3]);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
 /* The context's HIP stream (hipStream_t), for callers that interoperate: work enqueued on it after

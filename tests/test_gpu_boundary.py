@@ -284,8 +284,10 @@ def test_fast_division_and_sqrt_match_ieee():
 
 def test_rng_domain_shortcuts_exhaustive():
     """sqrt_rng (the unscaled sqrt) on every u01 value and every -2 log(u01), and the unguarded sin/cos
-    on both angle forms of raytracing.glsl, equal the general routines for all 2^32 RNG states."""
+    on both angle forms of raytracing.glsl, equal the general routines for all 2^32 RNG states; and
+    adjust_dir's Lambertian shortcut premise holds for all of them (a normal_dist radius is finite and
+    nonzero iff u01 is neither 0 nor 1; the angle's cosine is never 0)."""
     lib = _lib.load()
-    out = np.zeros(2, np.uint64)
+    out = np.zeros(3, np.uint64)
     _lib.check(lib.hrt_debug_math_check_rng(0, _lib.ptr(out)), "hrt_debug_math_check_rng")
-    assert out[0] == 0 and out[1] == 0, out
+    assert out[0] == 0 and out[1] == 0 and out[2] == 0, out
