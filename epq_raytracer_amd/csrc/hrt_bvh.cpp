@@ -263,26 +263,39 @@ void build_band_lists(BvhHost& out) {
     nh[k] = n * (1.0 / norm(n));
   }
   const int kDirRes = (int)out.dir_res, kDirCells = 6 * kDirRes * kDirRes;
+  // coarse-to-fine: a cell's candidates are its parent's entries whose band meets the cell's cap
+  // (the caps nest up to their 1e-4 rad widening, which cone_hits_band's caps all carry)
   constexpr int kCoarse = 8;
-  const int kSub = kDirRes / kCoarse;
+  const int kMid = std::min(kDirRes, 64), kSubMid = kMid / kCoarse, kSub = kDirRes / kMid;
   out.band_off.assign(kDirCells + 1, 0);
   std::vector<std::vector<uint32_t>> lists(kDirCells);
-  // one task per coarse cell: its candidates, then its kSub x kSub fine cells
+  auto cone_of = [](int f, int res, int iu, int iv) {
+    return cell_cone(f, -1.0 + 2.0 * iu / res, -1.0 + 2.0 * (iu + 1) / res, -1.0 + 2.0 * iv / res,
+                     -1.0 + 2.0 * (iv + 1) / res);
+  };
+  // one task per coarse cell: its candidates, then its mid cells', then their fine cells'
   auto task = [&](int t) {
     const int f = t / (kCoarse * kCoarse), cu = (t / kCoarse) % kCoarse, cv = t % kCoarse;
-    const Cone kc = cell_cone(f, -1.0 + 2.0 * cu / kCoarse, -1.0 + 2.0 * (cu + 1) / kCoarse,
-                              -1.0 + 2.0 * cv / kCoarse, -1.0 + 2.0 * (cv + 1) / kCoarse);
-    std::vector<uint32_t> coarse;
+    const Cone kc = cone_of(f, kCoarse, cu, cv);
+    std::vector<uint32_t> coarse, mid;
     for (uint32_t k = 0; k < out.n_prims; ++k)
       if (cone_hits_band(kc, nh[k])) coarse.push_back(k);
-    for (int su = 0; su < kSub; ++su) {
-      for (int sv = 0; sv < kSub; ++sv) {
-        const int iu = cu * kSub + su, iv = cv * kSub + sv;
-        const Cone fc = cell_cone(f, -1.0 + 2.0 * iu / kDirRes, -1.0 + 2.0 * (iu + 1) / kDirRes,
-                                  -1.0 + 2.0 * iv / kDirRes, -1.0 + 2.0 * (iv + 1) / kDirRes);
-        std::vector<uint32_t>& l = lists[((size_t)f * kDirRes + iu) * kDirRes + iv];
+    for (int mu = 0; mu < kSubMid; ++mu) {
+      for (int mv = 0; mv < kSubMid; ++mv) {
+        const int ju = cu * kSubMid + mu, jv = cv * kSubMid + mv;
+        const Cone mc = cone_of(f, kMid, ju, jv);
+        mid.clear();
         for (uint32_t k : coarse)
-          if (cone_hits_band(fc, nh[k])) l.push_back(k);
+          if (cone_hits_band(mc, nh[k])) mid.push_back(k);
+        for (int su = 0; su < kSub; ++su) {
+          for (int sv = 0; sv < kSub; ++sv) {
+            const int iu = ju * kSub + su, iv = jv * kSub + sv;
+            const Cone fc = cone_of(f, kDirRes, iu, iv);
+            std::vector<uint32_t>& l = lists[((size_t)f * kDirRes + iu) * kDirRes + iv];
+            for (uint32_t k : mid)
+              if (cone_hits_band(fc, nh[k])) l.push_back(k);
+          }
+        }
       }
     }
   };
@@ -297,17 +310,23 @@ void build_band_lists(BvhHost& out) {
   worker();
   for (auto& th : pool) th.join();
   for (int c = 0; c < kDirCells; ++c) out.band_off[c + 1] = out.band_off[c] + (uint32_t)lists[c].size();
-  out.band_list.reserve((size_t)out.band_off[kDirCells] * 2);
+  // 8 B per entry: the prim index and n / |n| in fixed point (hrt_bvh.h kBand*): the kernel's pre-check
+  // of d.n^ against the band, widened by the quantization error (encoded once per prim)
+  std::vector<uint32_t> enc((size_t)out.n_prims * 2);
+  for (uint32_t k = 0; k < out.n_prims; ++k) {
+    const float* n = &out.prims[(size_t)k * 16 + 12];
+    const double inv = 1.0 / norm(ld(n));
+    const int32_t qx = (int32_t)std::lround(n[0] * inv * kBandQx), qy = (int32_t)std::lround(n[1] * inv * kBandQyz),
+                  qz = (int32_t)std::lround(n[2] * inv * kBandQyz);
+    enc[2 * k] = k | ((uint32_t)qx & 0x3FFFu) << 18;
+    enc[2 * k + 1] = ((uint32_t)qy & 0xFFFFu) | ((uint32_t)qz & 0xFFFFu) << 16;
+  }
+  out.band_list.resize((size_t)out.band_off[kDirCells] * 2);
   for (int c = 0; c < kDirCells; ++c) {
+    uint32_t* w = out.band_list.data() + (size_t)out.band_off[c] * 2;
     for (uint32_t k : lists[c]) {
-      // 8 B: the prim index and n / |n| in fixed point (hrt_bvh.h kBand*): the kernel's pre-check of
-      // d.n^ against the band, widened by the quantization error
-      const float* n = &out.prims[(size_t)k * 16 + 12];
-      const double inv = 1.0 / norm(ld(n));
-      const int32_t qx = (int32_t)std::lround(n[0] * inv * kBandQx), qy = (int32_t)std::lround(n[1] * inv * kBandQyz),
-                    qz = (int32_t)std::lround(n[2] * inv * kBandQyz);
-      out.band_list.push_back(k | ((uint32_t)qx & 0x3FFFu) << 18);
-      out.band_list.push_back(((uint32_t)qy & 0xFFFFu) | ((uint32_t)qz & 0xFFFFu) << 16);
+      *w++ = enc[2 * k];
+      *w++ = enc[2 * k + 1];
     }
   }
 }

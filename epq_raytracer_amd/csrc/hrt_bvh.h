@@ -62,8 +62,11 @@ constexpr float kBandQErr = 7e-5f;
 // cell's list on every bounce) but ~linearly more entries per triangle (a triangle's band is a
 // great-circle strip).  256 up to 8K entries (island: 9 entries per list, 29 MB), 128 up to 32K, 64
 // above (profiles/r01p_*).
-constexpr int kDirResMax = 256;
-inline int dir_res_for(uint64_t entries) { return entries <= 8192 ? 256 : entries <= 32768 ? 128 : 64; }
+#ifndef HRT_DIR_RES_SMALL
+#define HRT_DIR_RES_SMALL 256
+#endif
+constexpr int kDirResMax = HRT_DIR_RES_SMALL;
+inline int dir_res_for(uint64_t entries) { return entries <= 8192 ? HRT_DIR_RES_SMALL : entries <= 32768 ? 128 : 64; }
 
 // Leaf size when HRT_OPT_BVH_LEAF_SIZE is 0 (auto): 2 for scenes BUNDLE_WQ takes (grouped nodes test
 // 4 children per visit, so smaller leaves cost few extra steps and save triangle pairs: island 3.42 ->
