@@ -1293,6 +1293,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
 #endif
+#ifndef HRT_WQ_BAND_FLAT
+#define HRT_WQ_BAND_FLAT 1  // the grazing-band lists scanned flattened over the wave (else per lane)
+#endif
 // Widest node group the kernel tests per stack entry (hrt_bvh.h kWqMaxWidth).  Measured (r02,
 // profiles/r02j_wq_groups_ab.jsonl): 8 slots ran the 4-wide image 9% slower (registers), and the
 // triangle stack of an 8-wide image does not fit the LDS; fully ordering the 4 slots (5
@@ -1471,7 +1474,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   // the irregular list and this lane's grazing-band list: per lane, as in BUNDLE_BVH
   uint32_t bkey = 0;
   float best_k = c.t * kOnePlus;
-  const BvhGlobal g{P.bvh_nodes, P.bvh_prims};
+  [[maybe_unused]] const BvhGlobal g{P.bvh_nodes, P.bvh_prims};
   for (uint32_t k = 0; k < P.bvh_n_irregular; ++k)
     if (sec) bvh_prim_test(P.bvh_irregular, k, mask, o, d, c, bkey, best_k);
 #if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 9
@@ -1499,11 +1502,78 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   }
   const float abs_t = P.bvh_abs_coef * R;
   uint32_t band_tests = 0, band_lmax = 0;
-#ifdef HRT_WQ_NOBAND
-  if (false) {
+  // the ray's closest hit so far (spheres, the irregular list) seeds its slot
+  const uint32_t id0 = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
+  wq.slot[lane] = ((unsigned long long)__float_as_uint(c.t) << 32) | id0;
+  uint32_t tc = 0, tri_pairs = 0, steps = 0;
+  // one step of 64 waiting triangle pairs (the band rounds' overflow guard)
+  [[maybe_unused]] auto tri_step64 = [&]() {
+    tc -= 64u;
+    const uint32_t e = wq.ts[tc + lane], r = e & 63u;
+    const unsigned long long rm =
+        ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
+        (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
+    wq_leaf_prim(P, wq, e >> 6, r, rm, shfl3(o, r), shfl3(d, r));
+    tri_pairs += 64u;
+    ++steps;
+  };
+#if HRT_WQ_BAND_FLAT
+  // Grazing band, flattened over the wave: the bounce lanes' direction-cell lists laid end to end
+  // (exclusive prefix pos of their lengths), 64 entries per round whatever the lists' lengths (the
+  // per-lane scan ran as long as the batch's longest list: 33 entries against 9.3 per lane on
+  // island).  Slot g's list is the last lane with pos <= g (a binary search over the lanes); an entry
+  // that passes its ray's pre-check becomes a (ray, prim) pair of the triangle steps, whose slot
+  // minimum is the per-lane scan's result.
+  if (__any(sec && mask)) {
+    uint32_t b0 = 0, n = 0;
+    const BandCheck bc(d, -kBandTau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
+    if (sec && mask) {
+      const uint32_t cell = dir_cell(d, P.bvh_dir_res);
+      b0 = P.bvh_band_off[cell];
+      n = P.bvh_band_off[cell + 1] - b0;
+    }
+    if (D && P.diag) {
+      dg.band_len += n;
+      band_lmax = n;
+    }
+    uint32_t pos = n;  // inclusive prefix, then exclusive
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)pos, sh, 64);
+      if (lane >= (uint32_t)sh) pos += t;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)pos, 63, 64);
+    pos -= n;
+    for (uint32_t base = 0; base < total; base += 64u) {
+      if (tc + 64u > P.wq_tcap) tri_step64();  // room for this round's pairs
+      const uint32_t gi = base + lane;
+      uint32_t lo = 0, pl = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1) {
+        const uint32_t pm = (uint32_t)__shfl((int)pos, (int)(lo + st), 64);
+        if (pm <= gi) {
+          lo += st;
+          pl = pm;
+        }
+      }
+      const uint32_t k = (uint32_t)__shfl((int)b0, (int)lo, 64) + (gi - pl);
+      BandCheck oc = bc;
+      oc.ds = shfl3(bc.ds, lo);
+      bool push = false;
+      uint32_t prim = 0;
+      if (gi < total) {
+        const uint2 q = P.bvh_band[k];
+        push = oc.in(q);
+        prim = BandCheck::prim(q);
+      }
+      const unsigned long long pb = __ballot(push);
+      if (push) wq.ts[tc + lanes_below(pb)] = (prim << 6) | lo;
+      tc += (uint32_t)__popcll(pb);
+      band_tests += push ? 1u : 0u;
+    }
+  }
 #else
   if (sec && mask) {
-#endif
     const uint32_t cell = dir_cell(d, P.bvh_dir_res);
     const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
     if (D && P.diag) {
@@ -1530,6 +1600,11 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       }
     }
   }
+  {  // the band's hits go to the slot
+    const uint32_t id1 = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
+    wq.slot[lane] = ((unsigned long long)__float_as_uint(c.t) << 32) | id1;
+  }
+#endif
 #if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 8
   if (sec && mask) {
     const float z = exp_zero();
@@ -1548,8 +1623,6 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   }
 #endif
   // pair traversal: the root is tested per lane, then (ray, node group) / (ray, triangle) pairs
-  const uint32_t id0 = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
-  wq.slot[lane] = ((unsigned long long)__float_as_uint(c.t) << 32) | id0;
   uint32_t rinfo = 0;
   bool rvis = false;
   if (sec && mask) {
@@ -1560,9 +1633,9 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   const uint32_t rcnt = rvis ? rinfo >> 27 : 0u;
   const unsigned long long rb = __ballot(rvis && rcnt == 0u);
   if (rvis && rcnt == 0u) wq.ns[lanes_below(rb)] = (rinfo << 6) | lane;  // inner root: its children's group
-  uint32_t nc = (uint32_t)__popcll(rb), tc = 0;
-  {  // leaf root (a scene of at most leaf-size triangles): its triangles
-    uint32_t pre = 0, tot = 0;
+  uint32_t nc = (uint32_t)__popcll(rb);
+  {  // leaf root (a scene of at most leaf-size triangles): its triangles, after any band pairs
+    uint32_t pre = tc, tot = 0;
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
       const unsigned long long bb = __ballot((rcnt >> b) & 1u);
@@ -1570,10 +1643,10 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       tot += (uint32_t)__popcll(bb) << b;
     }
     for (uint32_t j = 0; j < rcnt; ++j) wq.ts[pre + j] = (((rinfo & 0x07FFFFFFu) + j) << 6) | lane;
-    tc = tot;
+    tc += tot;
   }
   const uint32_t width = P.bvh_wq_width;  // the image's largest group
-  uint32_t node_pairs = 0, tri_pairs = 0, steps = 0;
+  uint32_t node_pairs = 0;
   while (nc | tc) {
     ++steps;
     // Step composition (wave-uniform): triangle pairs when >= 64 wait or no node pair is left; when
