@@ -77,9 +77,9 @@ __device__ __forceinline__ f3 get_ray_dir(const hrt_push_constants& pc, f3 c, ui
   return normalize(w);
 }
 
-// intersecting_aabb, raytracing.glsl:192-210, restated with its min/max quirks (:202, :206).
-__device__ __forceinline__ bool aabb_pass(const hrt_mesh& m, f3 o, f3 d) {
-  const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+// intersecting_aabb, raytracing.glsl:192-210, restated with its min/max quirks (:202, :206); inv =
+// (1/d.x, 1/d.y, 1/d.z) correctly rounded (computed once per ray for all meshes).
+__device__ __forceinline__ bool aabb_pass_inv(const hrt_mesh& m, f3 o, f3 inv) {
   float d_max = (((inv.x < 0.0f) ? m.min_point[0] : m.max_point[0]) - o.x) * inv.x;
   float d_min = (((inv.x < 0.0f) ? m.max_point[0] : m.min_point[0]) - o.x) * inv.x;
   if (d_max > 0.0f || d_min > 0.0f) return true;
@@ -89,6 +89,9 @@ __device__ __forceinline__ bool aabb_pass(const hrt_mesh& m, f3 o, f3 d) {
   d_max = gmax(d_max, (((inv.z < 0.0f) ? m.min_point[2] : m.max_point[2]) - o.z) * inv.z);
   d_min = gmax(d_min, (((inv.z < 0.0f) ? m.max_point[2] : m.min_point[2]) - o.z) * inv.z);
   return d_max > 0.0f || d_min > 0.0f;
+}
+__device__ __forceinline__ bool aabb_pass(const hrt_mesh& m, f3 o, f3 d) {
+  return aabb_pass_inv(m, o, mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z));
 }
 
 // Result of world_hit: closest distance and what produced it (kind 0 none, 1 sphere, 2 triangle).
@@ -1461,11 +1464,12 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   const hrt_push_constants& pc = P.pc;
   const uint32_t lane = threadIdx.x & 63;
   spheres_first(sc, pc, sec, o, d, c);
+  const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // the meshes' AABB tests and the traversal
   unsigned long long mask = 0ull;
   if (sec) {
     for (int m = 0; m < pc.num_meshes; ++m) {
       const hrt_mesh& mesh = sc.meshes[m];
-      if (aabb_pass(mesh, o, d)) {
+      if (aabb_pass_inv(mesh, o, inv)) {
         mask |= 1ull << m;
         tests += mesh.len;
       }
@@ -1492,7 +1496,6 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     exp_use((float)m2 + (float)t2);
   }
 #endif
-  const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   float R;
   {  // farthest root-box corner from the origin, rounded up
     const float4 R0 = wq.nodes[0], R1 = wq.nodes[1];
