@@ -445,8 +445,16 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   s.cam_capacity = (uint32_t)cap;
   // bounce-segment hierarchy (BUNDLE_BVH / BUNDLE_WQ)
   hrt::BvhHost bvh;
-  const uint32_t leaf = ctx->bvh_leaf ? ctx->bvh_leaf : hrt::auto_leaf_size(cap);
-  const bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, bvh, ctx->bvh_width);
+  // auto leaf size: 2, 3, then 4 for scenes BUNDLE_WQ takes -- the smallest whose grouped image leaves
+  // the LDS stacks kAutoLeafWqStack entries (island: 2; cave: 3, whose leaves of 2 need 104 KB of
+  // nodes); 4 above 8192 entries
+  uint32_t leaf = ctx->bvh_leaf ? ctx->bvh_leaf : hrt::auto_leaf_size(cap);
+  bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, bvh, ctx->bvh_width);
+  while (built && ctx->bvh_leaf == 0 && leaf < 4 &&
+         !(bvh.wq_ok && hrt::wq_stack_cap(bvh.wq_n_nodes, bvh.wq_width, leaf) >= hrt::kAutoLeafWqStack)) {
+    ++leaf;
+    built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, bvh, ctx->bvh_width);
+  }
   if (built) {
     auto up = [&](auto*& dst, const auto& v, const char* what) -> hrt_status {
       return alloc_upload(ctx, alloc, (void**)&dst, v.data(), v.size() * sizeof(v[0]), what);

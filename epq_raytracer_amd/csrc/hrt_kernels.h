@@ -88,6 +88,10 @@ hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint3
 // hrt_debug_math_check: fast division / sqrt paths vs the IEEE sequences (out[4] device counters).
 hipError_t launch_math_check(uint32_t n, uint32_t seed, unsigned long long* out, hipStream_t stream);
 hipError_t launch_math_check_rng(unsigned long long* out, hipStream_t stream);  // all 2^32 RNG states
+// BUNDLE_WQ's per-wave node-stack capacity for an image of n_nodes records with groups of `width` and
+// leaves of at most max_leaf triangles (0: does not fit the LDS)
+uint32_t wq_stack_cap(uint32_t n_nodes, uint32_t width, uint32_t max_leaf);
+constexpr uint32_t kAutoLeafWqStack = 512;  // auto leaf size: the smallest leaf whose image leaves this much
 hipError_t launch_convert(const uint32_t* src8, float4* dst32, const float4* src32, uint32_t* dst8, size_t npix,
                           hipStream_t stream);
 

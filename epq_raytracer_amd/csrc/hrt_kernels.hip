@@ -2504,6 +2504,7 @@ static inline unsigned blocks_for(size_t n) { return (unsigned)((n + 255) / 256)
 constexpr size_t kMaxLdsScene = 160 * 1024 - 64;  // dynamic LDS per CU, leaving room for the kernels' static LDS
 constexpr uint32_t kAutoCullTris = 256;   // BUNDLE_CULL from this many mesh triangles, BUNDLE below
 constexpr uint32_t kAutoBvhTris = 4096;   // BUNDLE_BVH from this many (profiles/r01d_bvh_scaling.log)
+constexpr uint32_t kAutoWqStack = 384;    // BUNDLE_WQ when its per-wave node stacks hold this many entries
 
 // BUNDLE_BVH_LDS footprint: triangles + nodes + entries + key bases.
 size_t bvh_lds_bytes(const TraceParams& p) {
@@ -2521,29 +2522,36 @@ uint32_t lds_block(uint32_t n) {
 
 // BUNDLE_WQ per-wave pair stacks: triangle stack 64 x (1 + 2 x largest leaf), node stack what is left of
 // the 160 KiB after the nodes (at most 1024 pairs, at least 128).  Returns the LDS bytes, 0 = no fit.
-size_t wq_lds_bytes(const TraceParams& p, uint32_t* ncap, uint32_t* tcap) {
-  if (!p.bvh_nodes || !p.bvh_wq_nodes || p.bvh_max_leaf > 4 || p.bvh_wq_width > kWqSlots) return 0;
+uint32_t wq_stack_cap(uint32_t n_nodes, uint32_t width, uint32_t max_leaf) {
+  if (max_leaf > 4 || width > kWqSlots || width < 2) return 0;
   // a node step pushes up to width x (largest leaf) triangle pairs per lane onto < 64 waiting ones
-  const size_t nodes = (size_t)p.bvh_wq_n_nodes * 48, t = 64u * (1u + p.bvh_wq_width * p.bvh_max_leaf);
+  const size_t nodes = (size_t)n_nodes * 48, t = 64u * (1u + width * max_leaf);
   if (nodes + 16 * (512 + 4 * (t + 128)) > kMaxLdsScene) return 0;
   const size_t per_wave = (kMaxLdsScene - nodes) / 16;
-  const uint32_t n = (uint32_t)std::min<size_t>(1024, ((per_wave - 512 - 4 * t) / 4) & ~(size_t)63);
+  return (uint32_t)std::min<size_t>(1024, ((per_wave - 512 - 4 * t) / 4) & ~(size_t)63);
+}
+
+size_t wq_lds_bytes(const TraceParams& p, uint32_t* ncap, uint32_t* tcap) {
+  if (!p.bvh_nodes || !p.bvh_wq_nodes) return 0;
+  const uint32_t n = wq_stack_cap(p.bvh_wq_n_nodes, p.bvh_wq_width, p.bvh_max_leaf);
+  if (n == 0) return 0;
+  const size_t t = 64u * (1u + p.bvh_wq_width * p.bvh_max_leaf);
   if (ncap) *ncap = n;
   if (tcap) *tcap = (uint32_t)t;
-  return nodes + 16 * (512 + 4 * ((size_t)n + t));
+  return (size_t)p.bvh_wq_n_nodes * 48 + 16 * (512 + 4 * ((size_t)n + t));
 }
 
 int resolve_variant(const TraceParams& p, int variant) {
   if (variant == HRT_KERNEL_AUTO) {
     // profiles/r01g_*: island 21.4 (LDS) vs 23.7 ms, cave 112 vs 120 ms; BVH from ~4K triangles.
-    // BUNDLE_WQ when its node stacks get >= 768 pairs (profiles/r01m_*: island, 1,024 pairs, 8.1 vs
-    // 15.6 ms; cave, 576 pairs with the 48 B node image: 36-39 vs 31-34 ms, r01o)
+    // BUNDLE_WQ when its node stacks get >= kAutoWqStack entries (r02, node groups: island 2.84 vs
+    // ~15 ms for BUNDLE_CULL_LDS; cave 17.3 ms at 384-entry stacks vs 20.2, profiles/r02p_cave_wq.txt)
     // A poor hierarchy (large overlapping triangles, HRT_SCENE_BVH_SAH_MILLI > 100) is left to the
     // wave-level culls: triangle soups of 256 / 1K / 4K / 16K run 2.5-5x faster culled
     // (profiles/r01p_soup_sweep.log).
     uint32_t ncap = 0;
     const bool good_bvh = p.bvh_nodes && p.bvh_sah_milli <= 100;
-    const bool wq = good_bvh && wq_lds_bytes(p, &ncap, nullptr) && ncap >= 768 && p.pc.num_meshes <= 64;
+    const bool wq = good_bvh && wq_lds_bytes(p, &ncap, nullptr) && ncap >= kAutoWqStack && p.pc.num_meshes <= 64;
     variant = p.cam_list_capacity < kAutoCullTris                   ? HRT_KERNEL_BUNDLE
               : wq                                                 ? HRT_KERNEL_BUNDLE_WQ
               : p.cam_list_capacity >= kAutoBvhTris && good_bvh    ? HRT_KERNEL_BUNDLE_BVH

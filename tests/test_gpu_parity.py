@@ -536,7 +536,8 @@ def test_large_scene_auto_picks_bvh():
 
 
 @pytest.mark.parametrize("scene,expect", [("soup1024", _lib.KERNEL_BUNDLE_CULL_LDS), ("soup4096", _lib.KERNEL_BUNDLE_CULL),
-                                          ("island", _lib.KERNEL_BUNDLE_WQ), ("island@2", _lib.KERNEL_BUNDLE_BVH)])
+                                          ("island", _lib.KERNEL_BUNDLE_WQ), ("cave", _lib.KERNEL_BUNDLE_WQ),
+                                          ("island@2", _lib.KERNEL_BUNDLE_BVH)])
 def test_auto_follows_hierarchy_quality(scene, expect):
     """AUTO reads the hierarchy's surface-area estimate (HRT_SCENE_BVH_SAH_MILLI): triangle soups (large
     overlapping triangles, ~500) are culled; island-like meshes (< 30) traverse the hierarchy."""
