@@ -735,9 +735,7 @@ __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool a
   bool ok;
   const Bundle b = tile_bundle(pc, active, centre, ok);
   if (!ok) return t;
-#ifndef HRT_AABB_LITERAL
   aabb_truth_table(P, t);
-#endif
   const uint32_t lane = threadIdx.x & 63;
   for (int m = 0; m < pc.num_meshes; ++m) {
     const uint32_t k0 = P.cam_start[m], k1 = k0 + P.cam_count[m];
@@ -1084,17 +1082,12 @@ __device__ __forceinline__ void bvh_tri_test(const float4& A, const float4& B, c
 __device__ __forceinline__ void bvh_prim_test(const float4* __restrict__ pr, uint32_t k, unsigned long long mask, f3 o,
                                               f3 d, Closest& c, uint32_t& bkey, float& best_k) {
   const float4 A = pr[4 * k], B = pr[4 * k + 1];
-#ifndef HRT_PRIM_TWO_TRIPS
   // all four record loads before the mesh filter (one memory round trip per test, not two: the
   // compiler would otherwise sink C and N below the branch)
   const float4 C = pr[4 * k + 2], N = pr[4 * k + 3];
   asm volatile("; record %0 %1" ::"v"(C.x), "v"(N.x));
-#endif
   const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
   if (!((mask >> m) & 1ull)) return;  // mesh failed its (quirky) AABB test for this lane
-#ifdef HRT_PRIM_TWO_TRIPS
-  const float4 C = pr[4 * k + 2], N = pr[4 * k + 3];
-#endif
   bvh_tri_test(A, B, C, N, __builtin_bit_cast(uint32_t, A.w), __builtin_bit_cast(uint32_t, C.w), m, o, d, c, bkey,
                best_k);
 }
@@ -1296,17 +1289,16 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
 #endif
-#ifndef HRT_WQ_BAND_FLAT
-#define HRT_WQ_BAND_FLAT 1  // the grazing-band lists scanned flattened over the wave (else per lane)
+#ifndef HRT_WQ_TRI_MIN
+#define HRT_WQ_TRI_MIN 64u  // a triangle step runs once this many triangle pairs wait (or no node pair is left)
 #endif
+
 // Widest node group the kernel tests per stack entry (hrt_bvh.h kWqMaxWidth).  Measured (r02,
 // profiles/r02j_wq_groups_ab.jsonl): 8 slots ran the 4-wide image 9% slower (registers), and the
 // triangle stack of an 8-wide image does not fit the LDS; fully ordering the 4 slots (5
 // compare-exchanges, HRT_WQ_FULLSORT) instead of only putting the nearest last (3) was 0.9% slower.
 constexpr uint32_t kWqSlots = 4;
-#ifndef HRT_WQ_FULLSORT
-#define HRT_WQ_FULLSORT 0
-#endif
+
 struct WqLds {
   const float4* nodes;        // BVH nodes (LDS copy)
   unsigned long long* slot;   // 64 per wave: closest hit so far per ray (owner lane)
@@ -1441,14 +1433,9 @@ __device__ __forceinline__ void wq_leaf_prim(const TraceParams& P, const WqLds& 
   const float4 A = pr[4 * k], B = pr[4 * k + 1], C = pr[4 * k + 2], N = pr[4 * k + 3];
   const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
   float dist;
-#ifdef HRT_WQ_MASK_FIRST
-  if (!((mask >> m) & 1ull)) return;  // mesh failed its (quirky) AABB test for this ray
-  if (wq_tri_accept(A, B, C, N, o, d, wq_slot_t(wq, r) * kOnePlus, dist)) {
-#else
   // the mesh filter (its quirky AABB test for this ray) joins the acceptance instead of leaving
   // first, so the four record loads issue together (one L2 round trip per triangle step, not two)
   if (wq_tri_accept(A, B, C, N, o, d, wq_slot_t(wq, r) * kOnePlus, dist) && ((mask >> m) & 1ull)) {
-#endif
     const uint32_t id = ((m << 26) | __builtin_bit_cast(uint32_t, C.w)) + 1u;
     atomicMin(&wq.slot[r], ((unsigned long long)__float_as_uint(dist) << 32) | id);
   }
@@ -1475,10 +1462,9 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       }
     }
   }
-  // the irregular list and this lane's grazing-band list: per lane, as in BUNDLE_BVH
+  // the irregular list: per lane, as in BUNDLE_BVH
   uint32_t bkey = 0;
   float best_k = c.t * kOnePlus;
-  [[maybe_unused]] const BvhGlobal g{P.bvh_nodes, P.bvh_prims};
   for (uint32_t k = 0; k < P.bvh_n_irregular; ++k)
     if (sec) bvh_prim_test(P.bvh_irregular, k, mask, o, d, c, bkey, best_k);
 #if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 9
@@ -1510,7 +1496,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   wq.slot[lane] = ((unsigned long long)__float_as_uint(c.t) << 32) | id0;
   uint32_t tc = 0, tri_pairs = 0, steps = 0;
   // one step of 64 waiting triangle pairs (the band rounds' overflow guard)
-  [[maybe_unused]] auto tri_step64 = [&]() {
+  auto tri_step64 = [&]() {
     tc -= 64u;
     const uint32_t e = wq.ts[tc + lane], r = e & 63u;
     const unsigned long long rm =
@@ -1520,7 +1506,6 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     tri_pairs += 64u;
     ++steps;
   };
-#if HRT_WQ_BAND_FLAT
   // Grazing band, flattened over the wave: the bounce lanes' direction-cell lists laid end to end
   // (exclusive prefix pos of their lengths), 64 entries per round whatever the lists' lengths (the
   // per-lane scan ran as long as the batch's longest list: 33 entries against 9.3 per lane on
@@ -1575,56 +1560,6 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       band_tests += push ? 1u : 0u;
     }
   }
-#else
-  if (sec && mask) {
-    const uint32_t cell = dir_cell(d, P.bvh_dir_res);
-    const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
-    if (D && P.diag) {
-      dg.band_len += b1 - b0;
-      band_lmax = b1 - b0;
-    }
-    const BandCheck bc(d, -kBandTau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
-    uint32_t k = b0;
-    for (; k + 4 <= b1; k += 4) {
-      const uint2 qs[4] = {P.bvh_band[k], P.bvh_band[k + 1], P.bvh_band[k + 2], P.bvh_band[k + 3]};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (bc.in(qs[j])) {
-          g.prim(BandCheck::prim(qs[j]), mask, o, d, c, bkey, best_k);
-          ++band_tests;
-        }
-      }
-    }
-    for (; k < b1; ++k) {
-      const uint2 q = P.bvh_band[k];
-      if (bc.in(q)) {
-        g.prim(BandCheck::prim(q), mask, o, d, c, bkey, best_k);
-        ++band_tests;
-      }
-    }
-  }
-  {  // the band's hits go to the slot
-    const uint32_t id1 = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
-    wq.slot[lane] = ((unsigned long long)__float_as_uint(c.t) << 32) | id1;
-  }
-#endif
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 8
-  if (sec && mask) {
-    const float z = exp_zero();
-    const f3 d2 = mk(d.x + z, d.y + z, d.z + z);
-    Closest c2 = c;
-    uint32_t bk2 = 0;
-    float bbk2 = best_k;
-    const uint32_t cell = dir_cell(d2, P.bvh_dir_res);
-    const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
-    const BandCheck bc(d2, -kBandTau - 2e-5f, 3e-5f);
-    for (uint32_t k = b0; k < b1; ++k) {
-      const uint2 q = P.bvh_band[k];
-      if (bc.in(q)) g.prim(BandCheck::prim(q), mask, o, d2, c2, bk2, bbk2);
-    }
-    exp_use(c2.t + (float)bk2);
-  }
-#endif
   // pair traversal: the root is tested per lane, then (ray, node group) / (ray, triangle) pairs
   uint32_t rinfo = 0;
   bool rvis = false;
@@ -1656,7 +1591,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     // both stacks are short, one mixed step takes them all (lanes [0, nn) node pairs, then triangles).
     // (Measured, r02: filling a short node step's idle lanes with triangle pairs, or running triangle
     // steps from 32 waiting pairs, was no faster: 3.699 / 3.722 vs 3.692 ms, profiles/r02g_ab.txt.)
-    const bool tri_step = tc >= 64u || nc == 0u;
+    const bool tri_step = tc >= HRT_WQ_TRI_MIN || nc == 0u;
     const bool mixed = HRT_WQ_MIXED && !tri_step && tc > 0u && nc + tc <= 64u;
     const uint32_t tn = tri_step ? min(64u, tc) : (mixed ? tc : 0u);
     const uint32_t nn = tri_step ? 0u : min(64u, nc);
@@ -1717,18 +1652,10 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
           }
         }
         // the nearest member in the last slot (pushed last = popped first)
-#if HRT_WQ_FULLSORT
-        wq_order(pk[0], pe[0], pk[1], pe[1]);
-        wq_order(pk[2], pe[2], pk[3], pe[3]);
-        wq_order(pk[0], pe[0], pk[2], pe[2]);
-        wq_order(pk[1], pe[1], pk[3], pe[3]);
-        wq_order(pk[1], pe[1], pk[2], pe[2]);
-#else
 #pragma unroll
         for (int st = 1; st < (int)kWqSlots; st *= 2)
 #pragma unroll
           for (int k = st - 1; k + st < (int)kWqSlots; k += 2 * st) wq_order(pk[k], pe[k], pk[k + st], pe[k + st]);
-#endif
       } else {  // finish the group's subtrees with a stackless walk (escape links)
         const uint32_t end = wq_escape(wq.nodes, fc + gcnt - 1u);
         uint32_t cur = fc;

@@ -211,6 +211,14 @@ def test_split_options_validated():
     for bad in (1, 127):
         with pytest.raises(Exception):
             ctx.set_option(_lib.OPT_WQ_NODE_CAP, bad)
+    for bad in (-1, 1, 5):  # group width 2..4
+        with pytest.raises(Exception):
+            ctx.set_option(_lib.OPT_BVH_WIDTH, bad)
+    for bad in (-1, 17):  # leaf size 0 (auto) or 1..16
+        with pytest.raises(Exception):
+            ctx.set_option(_lib.OPT_BVH_LEAF_SIZE, bad)
+    ctx.set_option(_lib.OPT_BVH_WIDTH, 3)
+    ctx.set_option(_lib.OPT_BVH_LEAF_SIZE, 0)
     with pytest.raises(Exception):
         ctx.set_option(_lib.OPT_PRIORITY, 3)
     with pytest.raises(Exception):
