@@ -9,6 +9,10 @@
 #include <cstring>
 #include <thread>
 
+#ifndef HRT_BVH_SWEEP
+#define HRT_BVH_SWEEP 1  // full-sweep SAH splits (0: 16 bins per axis)
+#endif
+
 namespace hrt {
 namespace {
 
@@ -119,6 +123,41 @@ struct Builder {
     bool leaf = n <= leaf_size;
     uint32_t mid = b + n / 2;
     if (!leaf) {
+#if HRT_BVH_SWEEP
+      // full-sweep SAH: every split between centroid-sorted entries on each axis
+      double best = HUGE_VAL;
+      int best_axis = -1;
+      uint32_t best_at = 0;
+      std::vector<double> right_area(n);
+      for (int k = 0; k < 3; ++k) {
+        std::sort(e.begin() + b, e.begin() + b + n, [&](const Entry& x, const Entry& y) {
+          const double cx = comp(x.centroid, k), cy = comp(y.centroid, k);
+          return cx < cy || (cx == cy && x.key < y.key);
+        });
+        Box acc;
+        for (uint32_t i = n; i-- > 1;) {
+          acc.grow(e[b + i].box);
+          right_area[i] = acc.area();
+        }
+        Box left;
+        for (uint32_t i = 1; i < n; ++i) {
+          left.grow(e[b + i - 1].box);
+          const double cost = left.area() * i + right_area[i] * (n - i);
+          if (cost < best) {
+            best = cost;
+            best_axis = k;
+            best_at = i;
+          }
+        }
+      }
+      if (best_axis >= 0) {
+        std::sort(e.begin() + b, e.begin() + b + n, [&](const Entry& x, const Entry& y) {
+          const double cx = comp(x.centroid, best_axis), cy = comp(y.centroid, best_axis);
+          return cx < cy || (cx == cy && x.key < y.key);
+        });
+        mid = b + best_at;
+      }
+#else
       // binned SAH over the centroid box, 16 bins per axis
       constexpr int kBins = 16;
       double best = HUGE_VAL;
@@ -170,6 +209,7 @@ struct Builder {
         mid = (uint32_t)(it - e.begin());
       }
       if (mid <= b || mid >= b + n) mid = b + n / 2;  // coincident centroids: split the range
+#endif
     }
 
     // box margin for a lane whose origin is within R of every scene vertex: mg = a + b R, from

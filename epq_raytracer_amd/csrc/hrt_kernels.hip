@@ -1692,14 +1692,22 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       pre += lanes_below(bb) << b;
       tot += (uint32_t)__popcll(bb) << b;
     }
-    uint32_t at = tc + pre;
+    if (tc + tot <= P.wq_tcap) {  // wave-uniform
+      uint32_t at = tc + pre;
 #pragma unroll
-    for (int k = 0; k < (int)kWqSlots; ++k) {
-      const uint32_t c = li[k] >> 27, first = li[k] & 0x07FFFFFFu;
-      for (uint32_t j = 0; j < c; ++j) wq.ts[at + j] = ((first + j) << 6) | r;
-      at += c;
+      for (int k = 0; k < (int)kWqSlots; ++k) {
+        const uint32_t c = li[k] >> 27, first = li[k] & 0x07FFFFFFu;
+        for (uint32_t j = 0; j < c; ++j) wq.ts[at + j] = ((first + j) << 6) | r;
+        at += c;
+      }
+      tc += tot;
+    } else {  // a burst of kept leaves beyond the triangle stack: each lane tests its own in place
+#pragma unroll
+      for (int k = 0; k < (int)kWqSlots; ++k) {
+        const uint32_t c = li[k] >> 27, first = li[k] & 0x07FFFFFFu;
+        for (uint32_t j = 0; j < c; ++j) wq_leaf_prim(P, wq, first + j, r, rm, ro, rd);
+      }
     }
-    tc += tot;
   }
   if (sec) {
     const unsigned long long s = wq.slot[lane];
@@ -2449,10 +2457,12 @@ uint32_t lds_block(uint32_t n) {
 
 // BUNDLE_WQ per-wave pair stacks: triangle stack 64 x (1 + 2 x largest leaf), node stack what is left of
 // the 160 KiB after the nodes (at most 1024 pairs, at least 128).  Returns the LDS bytes, 0 = no fit.
+// Triangle stack: 64 x (1 + 2 x largest leaf) pairs -- a node step's pushes onto < 64 waiting ones
+// when each lane keeps at most two leaves; a larger burst of a grouped step is tested in place.
+constexpr uint32_t wq_tri_cap(uint32_t max_leaf) { return 64u * (1u + 2u * max_leaf); }
 uint32_t wq_stack_cap(uint32_t n_nodes, uint32_t width, uint32_t max_leaf) {
   if (max_leaf > 4 || width > kWqSlots || width < 2) return 0;
-  // a node step pushes up to width x (largest leaf) triangle pairs per lane onto < 64 waiting ones
-  const size_t nodes = (size_t)n_nodes * 48, t = 64u * (1u + width * max_leaf);
+  const size_t nodes = (size_t)n_nodes * 48, t = wq_tri_cap(max_leaf);
   if (nodes + 16 * (512 + 4 * (t + 128)) > kMaxLdsScene) return 0;
   const size_t per_wave = (kMaxLdsScene - nodes) / 16;
   return (uint32_t)std::min<size_t>(1024, ((per_wave - 512 - 4 * t) / 4) & ~(size_t)63);
@@ -2462,7 +2472,7 @@ size_t wq_lds_bytes(const TraceParams& p, uint32_t* ncap, uint32_t* tcap) {
   if (!p.bvh_nodes || !p.bvh_wq_nodes) return 0;
   const uint32_t n = wq_stack_cap(p.bvh_wq_n_nodes, p.bvh_wq_width, p.bvh_max_leaf);
   if (n == 0) return 0;
-  const size_t t = 64u * (1u + p.bvh_wq_width * p.bvh_max_leaf);
+  const size_t t = wq_tri_cap(p.bvh_max_leaf);
   if (ncap) *ncap = n;
   if (tcap) *tcap = (uint32_t)t;
   return (size_t)p.bvh_wq_n_nodes * 48 + 16 * (512 + 4 * ((size_t)n + t));
