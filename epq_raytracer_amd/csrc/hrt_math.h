@@ -184,16 +184,16 @@ __device__ __forceinline__ float spec_cos(float x) {
   return c;
 }
 // The same for x in [0, 7] (the RNG's angles u * 2pi): the NaN / range guard always passes there.
+// The quadrant as selects and sign flips (no branches): odd q swaps the polynomials, q & 2 negates
+// the sine, (q + 1) & 2 the cosine -- the switch above, value for value.
 __device__ __forceinline__ void spec_sincos_angle(float x, float& s, float& c) {
   int q;
   const float r = spec_reduce(x, q);
   const float ps = sin_poly(r), pc = cos_poly(r);
-  switch (q & 3) {
-    case 0: s = ps; c = pc; break;
-    case 1: s = pc; c = -ps; break;
-    case 2: s = -ps; c = -pc; break;
-    default: s = -pc; c = ps; break;
-  }
+  const bool odd = (q & 1) != 0;
+  const uint32_t sn = ((uint32_t)q & 2u) << 30, cn = ((uint32_t)(q + 1) & 2u) << 30;
+  s = bitsf(fbits(odd ? pc : ps) ^ sn);
+  c = bitsf(fbits(odd ? ps : pc) ^ cn);
 }
 
 // ---- RNG: assets/raytracing.glsl:13-40 ------------------------------------------------------
