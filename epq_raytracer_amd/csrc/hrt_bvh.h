@@ -51,7 +51,10 @@ struct BvhHost {
   float abs_coef = 0.0f, rel_t = 0.0f;  // box-test t-slack: [-abs_coef R, best (1 + rel_t) + abs_coef R]
 };
 
-constexpr float kBandTau = 3e-3f;
+#ifndef HRT_BAND_TAU
+#define HRT_BAND_TAU 4.5e-3f
+#endif
+constexpr float kBandTau = HRT_BAND_TAU;
 // Grazing-band entries (8 B): prim index (18 bits, kBvhMaxEntries) | round(n^x * kBandQx) as a signed
 // 14-bit field << 18; round(n^y * kBandQyz) | round(n^z * kBandQyz) << 16, signed 16-bit fields.
 // |n^ - decoded| <= 0.5 / kBandQx in x, 0.5 / kBandQyz in y, z: |d.n^ - d.decoded| <= 6.2e-5 for |d| = 1,

@@ -17,7 +17,7 @@ import pytest
 
 from helpers import E, SceneCase, _lib
 
-TAU_G = np.float32(3e-3)   # hrt_bvh.h kBandTau
+TAU_G = np.float32(4.5e-3)   # hrt_bvh.h kBandTau
 DIR_RES_MAX = 256          # hrt_bvh.h kDirResMax (the scene's resolution comes back in counts[6])
 
 
