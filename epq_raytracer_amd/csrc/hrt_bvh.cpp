@@ -296,6 +296,57 @@ bool cone_hits_band(const Cone& k, V3 nhat) {
   return hi > -((double)kBandTau + 1e-5) && lo < 2e-5;
 }
 
+// The cell itself (a convex spherical quad): corners in order and its edges' planes.  The exact range
+// of d.nhat over the quad is at a corner, at an edge's interior critical point (nhat projected onto
+// the edge's great circle, when that point lies on the edge), or +-1 when +-nhat lies inside.
+struct Quad {
+  V3 c[4], m[4];  // unit corners; m[i] = c[i] x c[i+1] (the edge's plane, unnormalized)
+  double s[4];    // +1 / -1: the side of plane i the quad lies on
+};
+Quad cell_quad(int f, double u0, double u1, double v0, double v1) {
+  Quad q;
+  const double us[4] = {u0, u1, u1, u0}, vs[4] = {v0, v0, v1, v1};
+  for (int i = 0; i < 4; ++i) {
+    q.c[i] = face_dir(f, us[i], vs[i]);
+    q.c[i] = q.c[i] * (1.0 / norm(q.c[i]));
+  }
+  V3 ctr = face_dir(f, 0.5 * (u0 + u1), 0.5 * (v0 + v1));
+  for (int i = 0; i < 4; ++i) {
+    q.m[i] = cross(q.c[i], q.c[(i + 1) & 3]);
+    q.s[i] = dot(q.m[i], ctr) >= 0.0 ? 1.0 : -1.0;
+  }
+  return q;
+}
+// Is d.nhat in the grazing band (-kBandTau - 1e-5, 2e-5) for some d of the quad widened by 1e-4 rad
+// (the kernel's dir_cell rounding; moving d by an angle e moves d.nhat by at most e)?
+bool quad_hits_band(const Quad& q, V3 n) {
+  double hi = -2.0, lo = 2.0;
+  for (int i = 0; i < 4; ++i) {
+    const double v = dot(q.c[i], n);
+    hi = std::max(hi, v);
+    lo = std::min(lo, v);
+  }
+  bool in_p = true, in_m = true;
+  for (int i = 0; i < 4; ++i) {
+    const V3 a = q.c[i], b = q.c[(i + 1) & 3], m = q.m[i];
+    const double mm = dot(m, m);
+    const double side = q.s[i] * dot(m, n);
+    in_p = in_p && side >= 0.0;
+    in_m = in_m && side <= 0.0;
+    if (!(mm > 0.0)) continue;
+    const V3 pr = n - m * (dot(n, m) / mm);  // nhat projected onto the edge's great-circle plane
+    const double pl = norm(pr);
+    if (!(pl > 1e-12)) continue;
+    const V3 ph = pr * (1.0 / pl);
+    if (dot(cross(a, ph), m) >= 0.0 && dot(cross(ph, b), m) >= 0.0) hi = std::max(hi, pl);   // max on the arc
+    if (dot(cross(a, ph), m) <= 0.0 && dot(cross(ph, b), m) <= 0.0) lo = std::min(lo, -pl);  // -ph on the arc
+  }
+  if (in_p) hi = 1.0;
+  if (in_m) lo = -1.0;
+  constexpr double kWiden = 1e-4 + 1e-9;
+  return hi + kWiden > -((double)kBandTau + 1e-5) && lo - kWiden < 2e-5;
+}
+
 void build_band_lists(BvhHost& out) {
   std::vector<V3> nh(out.n_prims);
   for (uint32_t k = 0; k < out.n_prims; ++k) {
@@ -330,10 +381,11 @@ void build_band_lists(BvhHost& out) {
         for (int su = 0; su < kSub; ++su) {
           for (int sv = 0; sv < kSub; ++sv) {
             const int iu = ju * kSub + su, iv = jv * kSub + sv;
-            const Cone fc = cone_of(f, kDirRes, iu, iv);
+            const Quad fq = cell_quad(f, -1.0 + 2.0 * iu / kDirRes, -1.0 + 2.0 * (iu + 1) / kDirRes,
+                                      -1.0 + 2.0 * iv / kDirRes, -1.0 + 2.0 * (iv + 1) / kDirRes);
             std::vector<uint32_t>& l = lists[((size_t)f * kDirRes + iu) * kDirRes + iv];
             for (uint32_t k : mid)
-              if (cone_hits_band(fc, nh[k])) l.push_back(k);
+              if (quad_hits_band(fq, nh[k])) l.push_back(k);
           }
         }
       }
