@@ -171,6 +171,7 @@ void free_scene(hrt_context* ctx, SceneBufs& s, bool keep_rays) {
   if (!keep_rays) free_dev(ctx, s.rays);
   free_dev(ctx, s.spheres);
   free_dev(ctx, s.tris);
+  free_dev(ctx, s.tri_nhat);
   free_dev(ctx, s.meshes);
   free_dev(ctx, s.bvh_nodes);
   free_dev(ctx, s.bvh_wq_nodes);
@@ -431,6 +432,11 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
       (st = alloc_upload(ctx, alloc, (void**)&s.tris, tris, (size_t)n_tris * 64, "triangles")) != HRT_OK ||
       (st = alloc_upload(ctx, alloc, (void**)&s.meshes, meshes, (size_t)n_meshes * 80, "meshes")) != HRT_OK)
     return st;
+  {  // the hit normal of each triangle, once (resolve_hit reads it instead of normalizing per hit)
+    hipError_t e = alloc((void**)&s.tri_nhat, (size_t)(n_tris ? n_tris : 1) * sizeof(float4));
+    if (e == hipSuccess) e = hrt::launch_tri_normals(s.tris, s.tri_nhat, n_tris, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hrt_set_scene: triangle normals");
+  }
   uint64_t cap = 0;
   for (uint32_t m = 0; m < n_meshes; ++m) cap += meshes[m].len;
   if (cap > 0xFFFFFFFFull) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_set_scene: too many mesh triangles");
@@ -550,6 +556,7 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.rays = s.rays;
   p.spheres = s.spheres;
   p.tris = s.tris;
+  p.tri_nhat = s.tri_nhat;
   p.meshes = s.meshes;
   p.img8 = lane.trace8;
   p.img32 = lane.trace32;

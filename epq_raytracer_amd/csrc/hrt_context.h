@@ -43,6 +43,7 @@ struct SceneBufs {
   float4* rays = nullptr;
   hrt_sphere* spheres = nullptr;
   hrt_triangle* tris = nullptr;
+  float4* tri_nhat = nullptr;      // normalize(tri.normal) per triangle
   hrt_mesh* meshes = nullptr;
   float4* bvh_nodes = nullptr;     // BUNDLE_BVH hierarchy (hrt_bvh.h)
   float4* bvh_wq_nodes = nullptr;  // its 48 B node image for BUNDLE_WQ (nullptr above 65535 nodes)

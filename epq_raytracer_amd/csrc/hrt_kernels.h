@@ -14,6 +14,7 @@ struct TraceParams {
   const hrt_sphere* spheres;
   const hrt_triangle* tris;
   const hrt_mesh* meshes;
+  const float4* tri_nhat;        // per triangle: normalize(normal) (tri_normals at hrt_set_scene)
   uint32_t* img8;                // local_rows x W packed RGBA8 (RGBA8 mode) or nullptr
   float4* img32;                 // local_rows x W float4 (RGBA32F mode) or nullptr
   unsigned long long* counters;  // [0] segments, [1] triangle tests, [2] wave steps; nullptr = off
@@ -79,6 +80,7 @@ int resolve_variant(const TraceParams& p, int variant);  // the kernel an HRT_KE
 hipError_t launch_make_rays(float4* rays, uint32_t width, uint32_t height, const float first[3], const float px[3],
                             const float py[3], hipStream_t stream);
 hipError_t launch_clear(uint32_t* img8, float4* img32, size_t npix, hipStream_t stream);
+hipError_t launch_tri_normals(const hrt_triangle* tris, float4* nhat, uint32_t n, hipStream_t stream);
 hipError_t launch_accumulate(uint32_t* cur8, const uint32_t* new8, float4* cur32, const float4* new32, size_t npix,
                              uint32_t frame, hipStream_t stream);
 // Row-tile framebuffer assembly: gathered = parts x local_rows rows (rank-major), frame = height rows of

@@ -47,6 +47,7 @@ struct Scene {
   const hrt_sphere* __restrict__ spheres;
   const hrt_triangle* __restrict__ tris;
   const hrt_mesh* __restrict__ meshes;
+  const float4* __restrict__ nhat;  // normalize(tri.normal) per triangle (tri_normals, same arithmetic)
 };
 
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -167,7 +168,8 @@ __device__ __forceinline__ HitRecord resolve_hit(const Scene& sc, const Closest&
     h.normal = normalize(h.pos - ld3(s.centre));
     h.mat = &s.material;
   } else {
-    h.normal = normalize(ld3(sc.tris[c.idx].normal));
+    const float4 nh = sc.nhat[c.idx];  // = normalize(ld3(sc.tris[c.idx].normal)), computed once per scene
+    h.normal = mk(nh.x, nh.y, nh.z);
     h.mat = &sc.meshes[c.mesh].material;
   }
   return h;
@@ -306,7 +308,7 @@ __device__ __forceinline__ void lane_pixel(const TraceParams& P, uint32_t& x, ui
 
 // ---- literal variant: raytracing.glsl main (:355-389) with trace_ray's loop as written ----------
 __global__ __launch_bounds__(256) void trace_literal(TraceParams P) {
-  const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
+  const Scene sc{P.rays, P.spheres, P.tris, P.meshes, P.tri_nhat};
   const hrt_push_constants& pc = P.pc;
   uint32_t x, lr;
   lane_pixel(P, x, lr);
@@ -453,7 +455,7 @@ __device__ __forceinline__ Closest world_hit_brute(const Scene& sc, const Src& s
 // as raytracing.glsl:379-385); the wave iterates until every lane's last path has ended.
 template <class Src>
 __device__ __forceinline__ void trace_fused(const TraceParams& P, const Src& src, uint32_t x, uint32_t lr) {
-  const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
+  const Scene sc{P.rays, P.spheres, P.tris, P.meshes, P.tri_nhat};
   const hrt_push_constants& pc = P.pc;
   const uint32_t y = global_row(lr, P);
   uint32_t segs = 0, tests = 0;
@@ -1738,7 +1740,7 @@ template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, const CullSrc& csrc,
                                                   const BvhSrc& bsrc, uint32_t* list_lds, Coop& co,
                                                   uint32_t frame = 0) {
-  const Scene sc{P.rays, P.spheres, P.tris, P.meshes};
+  const Scene sc{P.rays, P.spheres, P.tris, P.meshes, P.tri_nhat};
   const hrt_push_constants& pc = P.pc;
   const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
   const uint32_t y = global_row(lr, P);
@@ -2291,6 +2293,14 @@ __global__ __launch_bounds__(256) void camera_lists(TraceParams P) {
 // ---- ray centres (create_ray_subbuffer's loop, src/raytrace_pipeline.rs:319-326) ------------------
 // (first + px * x) + py * y per component, each product and sum rounded as written (-ffp-contract=off):
 // the same bits as hrt_host_create_rays.
+// normalize(triangle normal) once per scene, as resolve_hit would per hit (raytracing.glsl:282 hit_normal)
+__global__ __launch_bounds__(256) void tri_normals(const hrt_triangle* tris, float4* nhat, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const f3 v = normalize(ld3(tris[i].normal));
+  nhat[i] = make_float4(v.x, v.y, v.z, 0.0f);
+}
+
 __global__ __launch_bounds__(256) void make_rays(float4* rays, uint32_t width, uint32_t height, float fx, float fy,
                                                  float fz, float pxx, float pxy, float pxz, float pyx, float pyy,
                                                  float pyz) {
@@ -2668,6 +2678,12 @@ hipError_t launch_make_rays(float4* rays, uint32_t width, uint32_t height, const
   const dim3 g((width + 15) / 16, (height + 15) / 16, 1);
   make_rays<<<g, 256, 0, stream>>>(rays, width, height, first[0], first[1], first[2], px[0], px[1], px[2], py[0],
                                    py[1], py[2]);
+  return hipGetLastError();
+}
+
+hipError_t launch_tri_normals(const hrt_triangle* tris, float4* nhat, uint32_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  tri_normals<<<(n + 255) / 256, 256, 0, stream>>>(tris, nhat, n);
   return hipGetLastError();
 }
 
