@@ -751,12 +751,14 @@ extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* 
       q.img32 = lane.trace32 ? reinterpret_cast<float4*>(ctx->frame_stack) : nullptr;
     }
     if ((st = launch_frames(ctx, q, ctx->stream, 0)) != HRT_OK) return st;
-    for (uint32_t f = 0; f < nf; ++f) {  // DiffusePipeline::next_frame(frame) in frame order
-      const uint32_t* t8 = nf > 1 && q.img8 ? q.img8 + f * np : lane.trace8;
-      const float4* t32 = nf > 1 && q.img32 ? q.img32 + f * np : lane.trace32;
-      HRT_HIP(ctx, hrt::launch_accumulate(ctx->accum8, t8, ctx->accum32, t32, np, q.pc.rng_offset + f, ctx->stream));
-      ctx->accumulates++;
-    }
+    // DiffusePipeline::next_frame(frame) for each frame, in frame order: one pass over the stack
+    if (nf > 1)
+      HRT_HIP(ctx, hrt::launch_accumulate_frames(ctx->accum8, q.img8, ctx->accum32, q.img32, np, nf, q.pc.rng_offset,
+                                                 ctx->stream));
+    else
+      HRT_HIP(ctx, hrt::launch_accumulate(ctx->accum8, lane.trace8, ctx->accum32, lane.trace32, np, q.pc.rng_offset,
+                                          ctx->stream));
+    ctx->accumulates += nf;
     if (nf > 1)  // the trace image holds the last frame, as after the per-frame loop
       HRT_HIP(ctx, hipMemcpyAsync(lane.image(), static_cast<const char*>(ctx->frame_stack) + (size_t)(nf - 1) * np * px_bytes,
                                   np * px_bytes, hipMemcpyDeviceToDevice, ctx->stream));

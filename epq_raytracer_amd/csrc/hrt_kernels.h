@@ -80,6 +80,9 @@ int resolve_variant(const TraceParams& p, int variant);  // the kernel an HRT_KE
 hipError_t launch_make_rays(float4* rays, uint32_t width, uint32_t height, const float first[3], const float px[3],
                             const float py[3], hipStream_t stream);
 hipError_t launch_clear(uint32_t* img8, float4* img32, size_t npix, hipStream_t stream);
+// the nf frames of a stack (image f at f * npix) folded into the accumulator as frames frame0 + f
+hipError_t launch_accumulate_frames(uint32_t* cur8, const uint32_t* stack8, float4* cur32, const float4* stack32,
+                                   size_t npix, uint32_t nf, uint32_t frame0, hipStream_t stream);
 hipError_t launch_tri_normals(const hrt_triangle* tris, float4* nhat, uint32_t n, hipStream_t stream);
 hipError_t launch_accumulate(uint32_t* cur8, const uint32_t* new8, float4* cur32, const float4* new32, size_t npix,
                              uint32_t frame, hipStream_t stream);

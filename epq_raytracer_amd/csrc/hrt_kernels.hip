@@ -2319,15 +2319,10 @@ __global__ __launch_bounds__(256) void clear_kernel(uint32_t* img8, float4* img3
   if (img32) img32[i] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
 }
 
-__global__ __launch_bounds__(256) void accumulate_rgba8(uint32_t* cur, const uint32_t* nw, size_t npix, uint32_t frame) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npix) return;
-  if (frame == 0) {
-    cur[i] = 255u << 24;
-    return;
-  }
+// image_combiner.glsl:22-43 for one pixel: frame 0 clears, frame k folds the new frame in.
+__device__ __forceinline__ uint32_t combine_rgba8(uint32_t pv, uint32_t nv, uint32_t frame) {
+  if (frame == 0) return 255u << 24;
   const float ff = (float)frame, ff1 = (float)(frame + 1u);
-  const uint32_t pv = cur[i], nv = nw[i];
   uint32_t out = 255u << 24;
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
@@ -2335,19 +2330,42 @@ __global__ __launch_bounds__(256) void accumulate_rgba8(uint32_t* cur, const uin
     const float nc = unorm8_to_float((nv >> (8 * ch)) & 255u);
     out |= unorm8((nc + prev * ff) / ff1) << (8 * ch);
   }
-  cur[i] = out;
+  return out;
+}
+__device__ __forceinline__ float4 combine_rgba32f(float4 p, float4 n, uint32_t frame) {
+  if (frame == 0) return make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+  const float ff = (float)frame, ff1 = (float)(frame + 1u);
+  return make_float4((n.x + p.x * ff) / ff1, (n.y + p.y * ff) / ff1, (n.z + p.z * ff) / ff1, 1.0f);
+}
+__global__ __launch_bounds__(256) void accumulate_rgba8(uint32_t* cur, const uint32_t* nw, size_t npix, uint32_t frame) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  cur[i] = combine_rgba8(frame == 0 ? 0u : cur[i], nw[i], frame);
+}
+// hrt_compute_n: the nf frames of one launch folded in frame order in one pass (frame frame0 + f is
+// image f of the stack): the per-frame combiner's arithmetic, pixel by pixel, with the accumulator
+// read and written once instead of once per frame.
+__global__ __launch_bounds__(256) void accumulate_frames_rgba8(uint32_t* cur, const uint32_t* stack, size_t npix,
+                                                             uint32_t nf, uint32_t frame0) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  uint32_t v = cur[i];
+  for (uint32_t f = 0; f < nf; ++f) v = combine_rgba8(v, stack[f * npix + i], frame0 + f);
+  cur[i] = v;
+}
+__global__ __launch_bounds__(256) void accumulate_frames_rgba32f(float4* cur, const float4* stack, size_t npix,
+                                                               uint32_t nf, uint32_t frame0) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  float4 v = cur[i];
+  for (uint32_t f = 0; f < nf; ++f) v = combine_rgba32f(v, stack[f * npix + i], frame0 + f);
+  cur[i] = v;
 }
 
 __global__ __launch_bounds__(256) void accumulate_rgba32f(float4* cur, const float4* nw, size_t npix, uint32_t frame) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= npix) return;
-  if (frame == 0) {
-    cur[i] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-    return;
-  }
-  const float ff = (float)frame, ff1 = (float)(frame + 1u);
-  const float4 p = cur[i], n = nw[i];
-  cur[i] = make_float4((n.x + p.x * ff) / ff1, (n.y + p.y * ff) / ff1, (n.z + p.z * ff) / ff1, 1.0f);
+  cur[i] = combine_rgba32f(frame == 0 ? make_float4(0.0f, 0.0f, 0.0f, 1.0f) : cur[i], nw[i], frame);
 }
 
 // format conversion for hrt_read_image
@@ -2678,6 +2696,16 @@ hipError_t launch_make_rays(float4* rays, uint32_t width, uint32_t height, const
   const dim3 g((width + 15) / 16, (height + 15) / 16, 1);
   make_rays<<<g, 256, 0, stream>>>(rays, width, height, first[0], first[1], first[2], px[0], px[1], px[2], py[0],
                                    py[1], py[2]);
+  return hipGetLastError();
+}
+
+hipError_t launch_accumulate_frames(uint32_t* cur8, const uint32_t* stack8, float4* cur32, const float4* stack32,
+                                   size_t npix, uint32_t nf, uint32_t frame0, hipStream_t stream) {
+  if (npix == 0 || nf == 0) return hipSuccess;
+  if (cur8)
+    accumulate_frames_rgba8<<<blocks_for(npix), 256, 0, stream>>>(cur8, stack8, npix, nf, frame0);
+  else
+    accumulate_frames_rgba32f<<<blocks_for(npix), 256, 0, stream>>>(cur32, stack32, npix, nf, frame0);
   return hipGetLastError();
 }
 
