@@ -583,6 +583,7 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.split_prio = ctx->split_prio;
   p.coop = ctx->coop;
   p.wq_ncap = ctx->wq_node_cap;  // request; launch_trace sizes the stacks
+  p.wq_tcap = ctx->debug_wq_tri_cap;  // (debug) request
   p.plan_valid = lane.plan_valid ? 1u : 0u;
   p.num_cus = ctx->grid_cus ? std::min(ctx->grid_cus, ctx->num_cus) : ctx->num_cus;
   const bool built = s.bvh_info[HRT_SCENE_BVH_BUILT] != 0;
@@ -1131,9 +1132,15 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       if (value < 0) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "fail-alloc index must be >= 0");
       ctx->debug_fail_alloc = value;
       return HRT_OK;
+    case HRT_DEBUG_OPT_WQ_TRI_CAP:
+      if (value != 0 && (value < 128 || value > (1 << 20)))
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "wq tri cap must be 0 (auto) or in [128, 2^20]");
+      ctx->debug_wq_tri_cap = (uint32_t)value;
+      return HRT_OK;
 #else
     case HRT_OPT_GRID_CUS:
     case HRT_DEBUG_OPT_FAIL_ALLOC:
+    case HRT_DEBUG_OPT_WQ_TRI_CAP:
       return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "debug option: only libhip_raytrace_debug.so accepts it");
 #endif
     default:

@@ -127,7 +127,8 @@ struct hrt_context {
   uint32_t num_cus = 0;
   uint32_t bvh_leaf = 0;  // HRT_OPT_BVH_LEAF_SIZE for the next hrt_set_scene (0 = auto, hrt_bvh.h)
   uint32_t bvh_width = 4;  // HRT_OPT_BVH_WIDTH (hrt_bvh.h kWqDefaultWidth) for the next hrt_set_scene
-  int64_t debug_fail_alloc = 0;  // debug build: fail the n-th device allocation of the next hrt_set_scene
+  int64_t debug_fail_alloc = 0;
+  uint32_t debug_wq_tri_cap = 0;  // debug build: HRT_DEBUG_OPT_WQ_TRI_CAP  // debug build: fail the n-th device allocation of the next hrt_set_scene
 
   int variant = 0;
   bool counters_on = true;

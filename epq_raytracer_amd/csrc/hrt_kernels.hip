@@ -2640,6 +2640,7 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
         q.split_factor = (uint64_t)tiles_of(p) * std::max(1u, p.n_frames) > 6ull * p.num_cus * 16u ? 2 : 3;
       const size_t lds = wq_lds_bytes(p, &q.wq_ncap, &q.wq_tcap);
       if (p.wq_ncap) q.wq_ncap = std::min(q.wq_ncap, std::max(128u, p.wq_ncap & ~63u));  // HRT_OPT_WQ_NODE_CAP
+      if (p.wq_tcap) q.wq_tcap = std::min(q.wq_tcap, std::max(128u, p.wq_tcap & ~63u));  // HRT_DEBUG_OPT_WQ_TRI_CAP
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
       if (p.diag || p.probe)
         trace_bundle_wq<true><<<p.num_cus, 1024, lds, stream>>>(q);

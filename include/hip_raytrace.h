@@ -237,7 +237,11 @@ typedef enum hrt_option {
   HRT_OPT_BVH_WIDTH = 15,
   /* libhip_raytrace_debug.so only (tests): the value-th device allocation of the next hrt_set_scene
    * fails with HRT_ERR_OUT_OF_MEMORY (0 = off) */
-  HRT_DEBUG_OPT_FAIL_ALLOC = 1001
+  HRT_DEBUG_OPT_FAIL_ALLOC = 1001,
+  /* libhip_raytrace_debug.so only (tests): BUNDLE_WQ's per-wave triangle-pair stack holds at most this
+   * many pairs (0 = what fits; else >= 128, rounded down to a multiple of 64): bursts of kept leaves
+   * beyond it are tested in place, the path the tests force with 128.  Results do not depend on it. */
+  HRT_DEBUG_OPT_WQ_TRI_CAP = 1002
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */

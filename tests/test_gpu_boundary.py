@@ -249,7 +249,8 @@ def test_production_library_rejects_debug_options():
     case = SceneCase("box", (16, 16), 1, 1)
     ctx = case.context()
     assert ctx.lib.hrt_debug_build() == 0
-    for key, value in ((_lib.OPT_PRIORITY, 2), (_lib.OPT_GRID_CUS, 4), (_lib.DEBUG_OPT_FAIL_ALLOC, 1)):
+    for key, value in ((_lib.OPT_PRIORITY, 2), (_lib.OPT_GRID_CUS, 4), (_lib.DEBUG_OPT_FAIL_ALLOC, 1),
+                       (_lib.DEBUG_OPT_WQ_TRI_CAP, 128)):
         with pytest.raises(_lib.HrtError, match="INVALID"):
             ctx.set_option(key, value)
     ctx.set_option(_lib.OPT_PRIORITY, 0)

@@ -155,6 +155,30 @@ def test_wq_pairs_bit_exact(scene, split, cap, width):
     ctx.close()
 
 
+@pytest.mark.parametrize("leaf", [0, 4])
+@pytest.mark.parametrize("scene", ["island", "cave", "ties"])
+def test_wq_triangle_stack_bursts_tested_in_place(scene, leaf):
+    """BUNDLE_WQ with its triangle-pair stack capped at 128 (debug library): most node steps' kept
+    leaves then do not fit and their lanes test them in place, and the band rounds drain the stack
+    early; frames and counters stay the oracle's."""
+    if scene == "ties":
+        case = _tie_soup()
+    else:
+        case = SceneCase(scene, (64, 48), 2, 8)
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context(variant=9, debug=True, options={_lib.DEBUG_OPT_WQ_TRI_CAP: 128, _lib.OPT_BVH_LEAF_SIZE: leaf})
+    for _ in range(2):
+        ctx.reset_stats()
+        ctx.trace(case.push())
+        st = ctx.stats()
+        img = ctx.read(_lib.IMG_TRACE)
+        assert np.array_equal(img, ref), mismatch_report(img, ref)
+        assert (st.segments, st.tri_tests) == (seg, tt)
+        if ctx.scene_info()["bvh_built"]:
+            assert st.last_kernel == 9
+    ctx.close()
+
+
 @pytest.mark.parametrize("split,coop,variant", [(8, 0, 7), (1, 1, 7), (0, 0, 9), (8, 0, 9)])
 def test_split_schedule_partition_and_scene_change(split, coop, variant):
     """Ragged row-tile partition (local rows not a multiple of 8) with every tile split (or run
