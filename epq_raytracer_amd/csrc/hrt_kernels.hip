@@ -1291,6 +1291,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
 #endif
+#ifndef HRT_WQ_BAND_CHUNK
+#define HRT_WQ_BAND_CHUNK 1  // band rounds whose loads are issued together (2 / 4 / 8 measured slower: r02t)
+#endif
 #ifndef HRT_WQ_TRI_MIN
 #define HRT_WQ_TRI_MIN 64u  // a triangle step runs once this many triangle pairs wait (or no node pair is left)
 #endif
@@ -1534,32 +1537,40 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     }
     const uint32_t total = (uint32_t)__shfl((int)pos, 63, 64);
     pos -= n;
-    for (uint32_t base = 0; base < total; base += 64u) {
-      if (tc + 64u > P.wq_tcap) tri_step64();  // room for this round's pairs
-      const uint32_t gi = base + lane;
-      uint32_t lo = 0, pl = 0;
+    // rounds in chunks of kBandChunk: every round's owner search and entry load issued before any
+    // round's check, so the chunk waits for its (mostly L2-missing) entry loads once
+    constexpr int kBandChunk = HRT_WQ_BAND_CHUNK;
+    for (uint32_t base = 0; base < total; base += 64u * kBandChunk) {
+      uint32_t own[kBandChunk];
+      uint2 q[kBandChunk];
 #pragma unroll
-      for (int st = 32; st > 0; st >>= 1) {
-        const uint32_t pm = (uint32_t)__shfl((int)pos, (int)(lo + st), 64);
-        if (pm <= gi) {
-          lo += st;
-          pl = pm;
+      for (int rr = 0; rr < kBandChunk; ++rr) {
+        const uint32_t gi = base + 64u * rr + lane;
+        uint32_t lo = 0, pl = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+          const uint32_t pm = (uint32_t)__shfl((int)pos, (int)(lo + st), 64);
+          if (pm <= gi) {
+            lo += st;
+            pl = pm;
+          }
         }
+        own[rr] = lo;
+        const uint32_t k = (uint32_t)__shfl((int)b0, (int)lo, 64) + (gi - pl);
+        q[rr] = gi < total ? P.bvh_band[k] : make_uint2(0u, 0u);
       }
-      const uint32_t k = (uint32_t)__shfl((int)b0, (int)lo, 64) + (gi - pl);
-      BandCheck oc = bc;
-      oc.ds = shfl3(bc.ds, lo);
-      bool push = false;
-      uint32_t prim = 0;
-      if (gi < total) {
-        const uint2 q = P.bvh_band[k];
-        push = oc.in(q);
-        prim = BandCheck::prim(q);
+#pragma unroll
+      for (int rr = 0; rr < kBandChunk; ++rr) {
+        if (base + 64u * rr >= total) break;  // wave-uniform
+        if (tc + 64u > P.wq_tcap) tri_step64();  // room for this round's pairs
+        BandCheck oc = bc;
+        oc.ds = shfl3(bc.ds, own[rr]);
+        const bool push = base + 64u * rr + lane < total && oc.in(q[rr]);
+        const unsigned long long pb = __ballot(push);
+        if (push) wq.ts[tc + lanes_below(pb)] = (BandCheck::prim(q[rr]) << 6) | own[rr];
+        tc += (uint32_t)__popcll(pb);
+        band_tests += push ? 1u : 0u;
       }
-      const unsigned long long pb = __ballot(push);
-      if (push) wq.ts[tc + lanes_below(pb)] = (prim << 6) | lo;
-      tc += (uint32_t)__popcll(pb);
-      band_tests += push ? 1u : 0u;
     }
   }
   // pair traversal: the root is tested per lane, then (ray, node group) / (ray, triangle) pairs
