@@ -1388,11 +1388,13 @@ __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& 
                                                 float t_hi, float& t_near) {
   const uint32_t w8 = __builtin_bit_cast(uint32_t, N2.x), w9 = __builtin_bit_cast(uint32_t, N2.y),
                  w10 = __builtin_bit_cast(uint32_t, N2.z);
-  const float x = half_lo(w8) * q.d.x + half_hi(w8) * q.d.y + half_lo(w9) * q.d.z;
+  // (fused: each rounding here is far inside the 2e-6 / 1e-6 slacks, and the host's margins carry 1e-6
+  // relative headroom over one rounding of a + b R)
+  const float x = __builtin_fmaf(half_lo(w9), q.d.z, __builtin_fmaf(half_hi(w8), q.d.y, half_lo(w8) * q.d.x));
   const float xa = fmaxf(fabsf(x) - (2e-6f + kWqAxisErr), 0.0f);
-  const float s_up = __builtin_amdgcn_sqrtf(fmaxf(1.0f - xa * xa, 0.0f)) + 1.2e-6f;
+  const float s_up = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-xa, xa, 1.0f), 0.0f)) + 1.2e-6f;
   if (HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back
-  const float mg = N0.w + N1.w * q.R;
+  const float mg = __builtin_fmaf(N1.w, q.R, N0.w);
   const float tx0 = __builtin_fmaf(N0.x - mg, q.inv.x, -q.oi.x), tx1 = __builtin_fmaf(N1.x + mg, q.inv.x, -q.oi.x);
   const float ty0 = __builtin_fmaf(N0.y - mg, q.inv.y, -q.oi.y), ty1 = __builtin_fmaf(N1.y + mg, q.inv.y, -q.oi.y);
   const float tz0 = __builtin_fmaf(N0.z - mg, q.inv.z, -q.oi.z), tz1 = __builtin_fmaf(N1.z + mg, q.inv.z, -q.oi.z);
