@@ -137,6 +137,33 @@ __device__ __forceinline__ float spec_log(float x) {
   return __builtin_fmaf(fk, 0.693359375f, r);
 }
 
+// spec_log on the RNG's values u01(h) = h 2^-32: 0 or in [2^-32, 1] -- never NaN, negative, infinite or
+// denormal, so only the zero case remains (checked over all 2^32 states, hrt_debug_math_check_rng).
+__device__ __forceinline__ float spec_log_u01(float x) {
+  uint32_t ix = fbits(x);
+  ix += 0x3f800000u - 0x3f3504f3u;
+  const int k = (int)(ix >> 23) - 0x7f;
+  ix = (ix & 0x007fffffu) + 0x3f3504f3u;
+  const float f = bitsf(ix) - 1.0f;
+  const float z = f * f;
+  float p = 7.0376836292e-2f;
+  p = __builtin_fmaf(p, f, -1.1514610310e-1f);
+  p = __builtin_fmaf(p, f, 1.1676998740e-1f);
+  p = __builtin_fmaf(p, f, -1.2420140846e-1f);
+  p = __builtin_fmaf(p, f, 1.4249322787e-1f);
+  p = __builtin_fmaf(p, f, -1.6668057665e-1f);
+  p = __builtin_fmaf(p, f, 2.0000714765e-1f);
+  p = __builtin_fmaf(p, f, -2.4999993993e-1f);
+  p = __builtin_fmaf(p, f, 3.3333331174e-1f);
+  float y = (p * f) * z;
+  const float fk = (float)k;
+  y = __builtin_fmaf(fk, -2.12194440e-4f, y);
+  y = __builtin_fmaf(z, -0.5f, y);
+  const float r = f + y;
+  const float l = __builtin_fmaf(fk, 0.693359375f, r);
+  return x == 0.0f ? -__builtin_inff() : l;
+}
+
 // S5: sin / cos.  Cody-Waite reduction by pi/2 (3 parts), odd/even polynomials on |r| <= pi/4.
 __device__ __forceinline__ float spec_reduce(float x, int& q) {
   const float j = __builtin_rintf(x * 0.636619772367581343f);
@@ -218,7 +245,7 @@ __device__ __forceinline__ float sqrt_rng(float x) { return sqrt_core(x); }
 
 __device__ __forceinline__ float normal_dist(uint32_t& state) {  // :28-33
   const float theta = 6.2831852f * u01(hash(state));  // 2 * 3.1415926 folded exactly
-  const float rho = sqrt_rng(-2.0f * spec_log(u01(hash(state))));
+  const float rho = sqrt_rng(-2.0f * spec_log_u01(u01(hash(state))));
   float s, c;
   spec_sincos_angle(theta, s, c);
   return rho * c;
