@@ -8,7 +8,8 @@
 //
 // Built twice: libhip_raytrace.so (production) and, with -DHRT_DEBUG_OPTIONS, libhip_raytrace_debug.so,
 // which also accepts the diagnostics-only options (HRT_OPT_PRIORITY = 2, HRT_OPT_GRID_CUS,
-// HRT_DEBUG_OPT_FAIL_ALLOC) that leave frames incomplete or inject failures.
+// HRT_DEBUG_OPT_FAIL_ALLOC, HRT_DEBUG_OPT_WQ_TRI_CAP) that leave frames incomplete, inject failures or
+// force rare paths.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -1799,7 +1799,11 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
           exp_use(d2.x + d2.y + d2.z);
         }
 #endif
+#ifdef HRT_EXP_ONE_NORMALIZE  // timing-only experiment (wrong frames): skip the caller's second normalize
+        p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, dir, 0, true};
+#else
         p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, normalize(dir), 0, true};
+#endif
       }
     }
     const bool prim = !done && p.bounce == 0;
