@@ -179,7 +179,8 @@ def main():
     kern_ms = st.total_trace_ms / max(st.traces, 1)  # per frame (a launch of f frames counts f traces)
     launches = -(-args.steps // fpl) if fpl > 1 else args.steps
     last_frame = frame - 1 - (args.realtime_frames + 6 if rt_ms is not None else 0)
-    kernel_sym = _lib.kernel_symbol(st.last_kernel, st.last_block)  # what HRT_KERNEL_AUTO resolved to
+    kernel_sym = _lib.kernel_symbol(st.last_kernel, st.last_block,  # what HRT_KERNEL_AUTO resolved to
+                                    node_r=_lib.wq_node_radius(ctx.scene_info()))
     if dist_on:
         t = torch.tensor([elapsed, kern_ms, rt_ms or 0.0], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

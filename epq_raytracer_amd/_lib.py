@@ -74,7 +74,7 @@ IMG_TRACE, IMG_ACCUM = 0, 1
 FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
 OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP, OPT_WQ_NODE_CAP, OPT_PROBE = 5, 6, 7, 8, 9, 10, 11
-OPT_FRAMES_PER_LAUNCH, OPT_OVERLAP, OPT_BUSY_SPLIT, OPT_BVH_WIDTH = 12, 13, 14, 15
+OPT_FRAMES_PER_LAUNCH, OPT_OVERLAP, OPT_BUSY_SPLIT, OPT_BVH_WIDTH, OPT_WQ_NODE_RADIUS = 12, 13, 14, 15, 16
 DEBUG_OPT_FAIL_ALLOC = 1001  # libhip_raytrace_debug.so only
 DEBUG_OPT_WQ_TRI_CAP = 1002  # libhip_raytrace_debug.so only
 COMM_ID_BYTES = 128
@@ -83,8 +83,18 @@ COMM_NONE, COMM_RCCL, COMM_RCCL_GROUP, COMM_DEVICE_COPY = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_LITERAL, KERNEL_BRUTE, KERNEL_BRUTE_LDS, KERNEL_BUNDLE, KERNEL_BUNDLE_CULL = 0, 1, 2, 3, 4, 5
 KERNEL_BUNDLE_BVH, KERNEL_BUNDLE_CULL_LDS, KERNEL_BUNDLE_BVH_LDS, KERNEL_BUNDLE_WQ = 6, 7, 8, 9
 # kernel symbol (as rocprofv3 names it) of a resolved hrt_kernel + workgroup size
-def kernel_symbol(kernel: int, block: int, diag: bool = False) -> str:
+NODE_RADIUS_MARGIN_MILLI = 100  # auto HRT_OPT_WQ_NODE_RADIUS: per-node R above this bvh_margin_milli (hrt_bvh.h)
+
+
+def wq_node_radius(scene_info: dict, option: int = 0) -> bool:
+    """Whether BUNDLE_WQ runs its per-node-radius kernel (trace_bundle_wq_nr) for this scene."""
+    return option == 2 or (option == 0 and scene_info.get("bvh_margin_milli", 0) > NODE_RADIUS_MARGIN_MILLI)
+
+
+def kernel_symbol(kernel: int, block: int, diag: bool = False, node_r: bool = False) -> str:
     d = "true" if diag else "false"
+    if kernel == 9 and node_r:
+        return f"void hrt::trace_bundle_wq_nr<{d}>(hrt::TraceParams)"
     if kernel in (1, 2, 3):
         return "hrt::" + {1: "trace_literal", 2: "trace_brute", 3: "trace_brute_lds"}[kernel] + "(hrt::TraceParams)"
     if kernel == 7:
@@ -101,7 +111,7 @@ DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounc
               "shade_cycles", "bounce_stage2", "bounce_front", "bvh_trips",
               "bvh_leaf_trips", "band_scan_max", "band_scan_len")
 SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh_built", "bvh_band_entries",
-                    "bvh_sah_milli")
+                    "bvh_sah_milli", "bvh_margin_milli")
 
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).
 EXPORTED_SYMBOLS = (

@@ -483,6 +483,7 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   s.bvh_info[HRT_SCENE_BVH_BUILT] = built ? 1u : 0u;
   s.bvh_info[HRT_SCENE_BVH_BAND_ENTRIES] = (uint32_t)(bvh.band_list.size() / 2);
   s.bvh_info[HRT_SCENE_BVH_SAH_MILLI] = (uint32_t)std::min(1e9, bvh.sah_tri_frac * 1000.0 + 0.5);
+  s.bvh_info[HRT_SCENE_BVH_MARGIN_MILLI] = (uint32_t)std::min(1e9, bvh.margin_frac * 1000.0 + 0.5);
   s.bvh_abs_coef = bvh.abs_coef;
   s.bvh_rel_t = bvh.rel_t;
   s.bvh_dir_res = bvh.dir_res;
@@ -605,6 +606,8 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.bvh_n_nodes = s.bvh_info[HRT_SCENE_BVH_NODES];
   p.bvh_abs_coef = s.bvh_abs_coef;
   p.bvh_rel_t = s.bvh_rel_t;
+  p.bvh_node_r = ctx->wq_node_radius == 2 ||
+                 (ctx->wq_node_radius == 0 && s.bvh_info[HRT_SCENE_BVH_MARGIN_MILLI] > hrt::kNodeRadiusMarginMilli);
   p.bvh_n_irregular = s.bvh_info[HRT_SCENE_BVH_IRREGULAR];
   p.bvh_max_leaf = s.bvh_built_leaf;
   p.n_frames = 1;
@@ -1118,6 +1121,10 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       if (value < 2 || value > (int64_t)hrt::kWqMaxWidth)
         return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "BVH width must be in [2, 4]");
       ctx->bvh_width = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_WQ_NODE_RADIUS:
+      if (value < 0 || value > 2) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "wq node radius must be 0 (auto), 1 or 2");
+      ctx->wq_node_radius = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_BVH_LEAF_SIZE:
       if (value < 0 || value > hrt::kBvhMaxLeafCount)

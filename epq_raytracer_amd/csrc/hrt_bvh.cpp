@@ -606,6 +606,17 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
       if (info >> 27) tests += (info >> 27) * (root > 0.0 ? area(k) / root : 1.0);
     }
     out.sah_tri_frac = tests / out.n_prims;
+    // how wide the box margins a + b R are at R = the scene's diagonal (HRT_SCENE_BVH_MARGIN_MILLI)
+    const float* r0 = &out.nodes[0];
+    const double R = std::sqrt((double)(r0[4] - r0[0]) * (r0[4] - r0[0]) + (double)(r0[5] - r0[1]) * (r0[5] - r0[1]) +
+                               (double)(r0[6] - r0[2]) * (r0[6] - r0[2]));
+    double msum = 0.0;
+    for (uint32_t k = 0; k < out.n_nodes; ++k) {
+      const float* r = &out.nodes[(size_t)k * 16];
+      const double ext = std::max({(double)r[4] - r[0], (double)r[5] - r[1], (double)r[6] - r[2], 1e-30});
+      msum += ((double)r[3] + (double)r[7] * R) / ext;
+    }
+    out.margin_frac = out.n_nodes ? msum / out.n_nodes : 0.0;
   }
   out.dir_res = (uint32_t)dir_res_for(out.n_prims);
   build_band_lists(out);

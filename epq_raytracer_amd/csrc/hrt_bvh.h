@@ -41,6 +41,7 @@ struct BvhHost {
   std::vector<uint32_t> band_off;   // 6 dir_res^2 + 1 offsets into band_list
   uint32_t dir_res = 64;            // direction cells per face edge (dir_res_for)
   double sah_tri_frac = 0.0;        // expected leaf triangle tests of a uniform random ray / entries
+  double margin_frac = 0.0;         // mean over nodes of (a + b R_scene) / the box's largest extent
   std::vector<uint32_t> band_list;  // 2 words per entry: prim | n^x << 18, n^y | n^z << 16 (kBand*)
   std::vector<float> wq_nodes;      // BUNDLE_WQ's 48 B node image (make_wq_nodes)
   bool wq_ok = false;               // the image exists (fewer than 65536 nodes)
@@ -50,6 +51,10 @@ struct BvhHost {
   double rho_max = 0.0;
   float abs_coef = 0.0f, rel_t = 0.0f;  // box-test t-slack: [-abs_coef R, best (1 + rel_t) + abs_coef R]
 };
+
+// auto HRT_OPT_WQ_NODE_RADIUS: per-node R above this HRT_SCENE_BVH_MARGIN_MILLI (island 26 / island@4 69:
+// scene-wide R; cave 197: per node, 8.54 -> 7.38 ms per frame; island with per-node R 2.33 -> 2.39 ms)
+constexpr uint32_t kNodeRadiusMarginMilli = 100;
 
 #ifndef HRT_BAND_TAU
 #define HRT_BAND_TAU 4.5e-3f

@@ -69,6 +69,7 @@ struct TraceParams {
   // rng_offset + f and writes img8 / img32 + f * frame_stride pixels.  0 or 1: one frame.
   uint32_t n_frames;
   size_t frame_stride;
+  uint32_t bvh_node_r;  // BUNDLE_WQ: trace_bundle_wq_nr, box margins with a per-node R (HRT_OPT_WQ_NODE_RADIUS)
 };
 
 // Per device, once: the dynamic-LDS limits of the persistent kernels (hipFuncSetAttribute).

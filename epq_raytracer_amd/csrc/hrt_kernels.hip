@@ -1384,6 +1384,7 @@ __device__ __forceinline__ WqRay wq_ray(f3 o, f3 d, f3 inv, float R, float abs_t
 // the 1e-6 relative slack and 2 sig on the interval test (one fma instead of a subtract and a
 // multiply per bound: island 3.242 -> 3.228 ms, profiles/r02k_node_test_ab.txt).  inv = +-inf gives
 // NaN -> visit.  (Measured and dropped: d.axis from binary16 d with v_dot2_f32_f16, 3.345 ms.)
+template <bool NodeR>
 __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& N1, const float4& N2, const WqRay& q,
                                                 float t_hi, float& t_near) {
   const uint32_t w8 = __builtin_bit_cast(uint32_t, N2.x), w9 = __builtin_bit_cast(uint32_t, N2.y),
@@ -1394,7 +1395,15 @@ __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& 
   const float xa = fmaxf(fabsf(x) - (2e-6f + kWqAxisErr), 0.0f);
   const float s_up = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-xa, xa, 1.0f), 0.0f)) + 1.2e-6f;
   if (HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back
-  const float mg = __builtin_fmaf(N1.w, q.R, N0.w);
+  float Rm = q.R;
+  if constexpr (NodeR) {  // trace_bundle_wq_nr (HRT_OPT_WQ_NODE_RADIUS)
+    // R for this member: the ray origin's distance to the farthest corner of its box (every vertex
+    // below lies in the box), x1.0001 over the roundings and the hardware square root
+    const float fx = fmaxf(q.o.x - N0.x, N1.x - q.o.x), fy = fmaxf(q.o.y - N0.y, N1.y - q.o.y),
+                fz = fmaxf(q.o.z - N0.z, N1.z - q.o.z);
+    Rm = fminf(__builtin_amdgcn_sqrtf(__builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx))) * 1.0001f, q.R);
+  }
+  const float mg = __builtin_fmaf(N1.w, Rm, N0.w);
   const float tx0 = __builtin_fmaf(N0.x - mg, q.inv.x, -q.oi.x), tx1 = __builtin_fmaf(N1.x + mg, q.inv.x, -q.oi.x);
   const float ty0 = __builtin_fmaf(N0.y - mg, q.inv.y, -q.oi.y), ty1 = __builtin_fmaf(N1.y + mg, q.inv.y, -q.oi.y);
   const float tz0 = __builtin_fmaf(N0.z - mg, q.inv.z, -q.oi.z), tz1 = __builtin_fmaf(N1.z + mg, q.inv.z, -q.oi.z);
@@ -1452,7 +1461,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
 
-template <bool D>
+template <bool D, bool NodeR>
 __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const TraceParams& P, const WqLds& wq, bool sec,
                                                     f3 o, f3 d, uint32_t& tests, Closest& c, Diag& dg) {
   const hrt_push_constants& pc = P.pc;
@@ -1645,7 +1654,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         auto member = [&](const float4& N0, const float4& N1, const float4& N2, int k) {
           float tnear;
           const uint32_t inf = __builtin_bit_cast(uint32_t, N2.w);
-          if (wq_member_visit(N0, N1, N2, rq, t_hi, tnear)) {
+          if (wq_member_visit<NodeR>(N0, N1, N2, rq, t_hi, tnear)) {
             if (inf >> 27) {
               li[k] = inf;
             } else {
@@ -1747,7 +1756,9 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 // at least sec_batch lanes wait or no primary segment is left in the wave, then all waiting lanes run
 // their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
 
-enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2, kBounceWq = 3 };
+// kBounceWqR: BUNDLE_WQ with node margins from each member's own R (HRT_OPT_WQ_NODE_RADIUS = 2)
+enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2, kBounceWq = 3, kBounceWqR = 4 };
+constexpr bool is_wq(int b) { return b == kBounceWq || b == kBounceWqR; }
 
 template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, const CullSrc& csrc,
@@ -1843,17 +1854,17 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     }
     if (D && P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
-      if constexpr (Bounce == kBounceWq) {
+      if constexpr (is_wq(Bounce)) {
 #if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 5
         const Closest c_in = c;
 #endif
-        world_hit_bounce_wq<D>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
+        world_hit_bounce_wq<D, Bounce == kBounceWqR>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
 #if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 5
         {
           const float z = exp_zero();
           Closest c2 = c_in;
           uint32_t t2 = 0;
-          world_hit_bounce_wq<D>(sc, P, bsrc, sec, p.pos, mk(p.dir.x + z, p.dir.y + z, p.dir.z + z), t2, c2, dg);
+          world_hit_bounce_wq<D, Bounce == kBounceWqR>(sc, P, bsrc, sec, p.pos, mk(p.dir.x + z, p.dir.y + z, p.dir.z + z), t2, c2, dg);
           exp_use(c2.t + (float)t2 + (float)c2.idx);
         }
 #endif
@@ -1912,11 +1923,11 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicMax(&rec[0], (unsigned long long)(__builtin_readcyclecounter() - tile_t0));  // slowest item of a split tile
     // bounce batches | (BUNDLE_WQ) pair steps << 32
     atomicAdd(&rec[1], (unsigned long long)dg.sec_iters |
-                           (Bounce == kBounceWq ? (unsigned long long)dg.bvh_trips << 32 : 0ull));
-    if (Bounce != kBounceBvh && Bounce != kBounceWq) atomicAdd(&rec[2], (unsigned long long)dg.sec_survivors);
+                           (is_wq(Bounce) ? (unsigned long long)dg.bvh_trips << 32 : 0ull));
+    if (Bounce != kBounceBvh && !is_wq(Bounce)) atomicAdd(&rec[2], (unsigned long long)dg.sec_survivors);
     atomicAdd(&rec[3], (unsigned long long)dg.cyc_sec);
   }
-  if (D && P.tile_cycles && (Bounce == kBounceBvh || Bounce == kBounceWq) && active) {
+  if (D && P.tile_cycles && (Bounce == kBounceBvh || is_wq(Bounce)) && active) {
     // BUNDLE_BVH: the tile's per-lane node visits, summed | (leaf + band triangle tests) << 32
     const uint32_t tiles_x = (pc.width + 7) / 8;
     atomicAdd(P.tile_cycles + 4 * ((lr / 8) * tiles_x + x / 8) + 2,
@@ -1939,7 +1950,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[5], (unsigned long long)dg.sec_survivors);
     atomicAdd(&P.diag[6], (unsigned long long)dg.sec_lanes);
   }
-  if (D && P.diag && (Bounce == kBounceBvh || Bounce == kBounceWq)) {
+  if (D && P.diag && (Bounce == kBounceBvh || is_wq(Bounce))) {
     atomicAdd(&P.diag[7], (unsigned long long)dg.bvh_visits);
     atomicAdd(&P.diag[8], (unsigned long long)dg.bvh_prims);
     atomicAdd(&P.diag[9], (unsigned long long)dg.bvh_band);
@@ -2210,20 +2221,29 @@ __global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
 
 // BUNDLE_WQ: the hierarchy's nodes in LDS, one pair-stack region per wave after them (persistent
 // 1024-thread workgroups).  Dynamic LDS: [nodes x 48 B][16 x (64 slots x 8 B, wq_ncap + wq_tcap words)].
+// (one body, two kernels: a __device__ wrapper taking P by reference changes the island kernel's
+// register allocation and cost 0.6%)
+#define HRT_WQ_KERNEL_BODY(BOUNCE)                                                                              \
+  {                                                                                                             \
+    const uint32_t nn = P.bvh_wq_n_nodes;                                                                       \
+    float4* nodes = lds_tris;                                                                                   \
+    for (uint32_t k = threadIdx.x; k < 3 * nn; k += 1024) nodes[k] = P.bvh_wq_nodes[k];                         \
+    char* base =                                                                                                \
+        reinterpret_cast<char*>(nodes + 3 * nn) + (size_t)(threadIdx.x >> 6) * (512 + 4 * (P.wq_ncap + P.wq_tcap)); \
+    const WqLds wq{nodes, reinterpret_cast<unsigned long long*>(base), reinterpret_cast<uint32_t*>(base + 512),  \
+                   reinterpret_cast<uint32_t*>(base + 512) + P.wq_ncap, P.wq_ncap};                            \
+    __syncthreads();                                                                                            \
+    const float4* T = reinterpret_cast<const float4*>(P.tris);                                                  \
+    tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f) {           \
+      trace_fused_split<BOUNCE, D>(P, x, lr, CullGlobal{T, to_const(T)}, wq, nullptr, co, f);                   \
+    });                                                                                                         \
+  }
 template <bool D>
-__global__ __launch_bounds__(1024) void trace_bundle_wq(TraceParams P) {
-  const uint32_t nn = P.bvh_wq_n_nodes;
-  float4* nodes = lds_tris;
-  for (uint32_t k = threadIdx.x; k < 3 * nn; k += 1024) nodes[k] = P.bvh_wq_nodes[k];
-  char* base = reinterpret_cast<char*>(nodes + 3 * nn) + (size_t)(threadIdx.x >> 6) * (512 + 4 * (P.wq_ncap + P.wq_tcap));
-  const WqLds wq{nodes, reinterpret_cast<unsigned long long*>(base), reinterpret_cast<uint32_t*>(base + 512),
-                 reinterpret_cast<uint32_t*>(base + 512) + P.wq_ncap, P.wq_ncap};
-  __syncthreads();
-  const float4* T = reinterpret_cast<const float4*>(P.tris);
-  tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f) {
-    trace_fused_split<kBounceWq, D>(P, x, lr, CullGlobal{T, to_const(T)}, wq, nullptr, co, f);
-  });
-}
+__global__ __launch_bounds__(1024) void trace_bundle_wq(TraceParams P) HRT_WQ_KERNEL_BODY(kBounceWq)
+// the same with per-member R in the node margins (TraceParams::bvh_node_r, HRT_OPT_WQ_NODE_RADIUS)
+template <bool D>
+__global__ __launch_bounds__(1024) void trace_bundle_wq_nr(TraceParams P) HRT_WQ_KERNEL_BODY(kBounceWqR)
+#undef HRT_WQ_KERNEL_BODY
 
 // BUNDLE_BVH with the hierarchy and the triangle image in LDS (persistent 1024-thread workgroups).
 // Dynamic LDS: [n_tris x 48 B triangles][nodes x 64 B][prims x 4 B entries][meshes x 4 B key bases].
@@ -2596,7 +2616,9 @@ hipError_t ensure_kernel_attributes(int device) {
                             reinterpret_cast<const void*>(&trace_bundle_bvh_lds<false>),
                             reinterpret_cast<const void*>(&trace_bundle_bvh_lds<true>),
                             reinterpret_cast<const void*>(&trace_bundle_wq<false>),
-                            reinterpret_cast<const void*>(&trace_bundle_wq<true>)};
+                            reinterpret_cast<const void*>(&trace_bundle_wq<true>),
+                            reinterpret_cast<const void*>(&trace_bundle_wq_nr<false>),
+                            reinterpret_cast<const void*>(&trace_bundle_wq_nr<true>)};
   hipError_t e;
   for (const void* f : brute)
     if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsScene)) != hipSuccess)
@@ -2661,10 +2683,16 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
       if (p.wq_ncap) q.wq_ncap = std::min(q.wq_ncap, std::max(128u, p.wq_ncap & ~63u));  // HRT_OPT_WQ_NODE_CAP
       if (p.wq_tcap) q.wq_tcap = std::min(q.wq_tcap, std::max(128u, p.wq_tcap & ~63u));  // HRT_DEBUG_OPT_WQ_TRI_CAP
       if (hipError_t e = prepare_schedule(q, stream); e != hipSuccess) return e;
-      if (p.diag || p.probe)
+      if (p.bvh_node_r) {
+        if (p.diag || p.probe)
+          trace_bundle_wq_nr<true><<<p.num_cus, 1024, lds, stream>>>(q);
+        else
+          trace_bundle_wq_nr<false><<<p.num_cus, 1024, lds, stream>>>(q);
+      } else if (p.diag || p.probe) {
         trace_bundle_wq<true><<<p.num_cus, 1024, lds, stream>>>(q);
-      else
+      } else {
         trace_bundle_wq<false><<<p.num_cus, 1024, lds, stream>>>(q);
+      }
       *block_out = 1024;
       break;
     }

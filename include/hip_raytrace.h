@@ -235,6 +235,12 @@ typedef enum hrt_option {
    * binary tree, 3 or 4 = groups of up to that many collapsed from it; default 4).  Results do not
    * depend on it. */
   HRT_OPT_BVH_WIDTH = 15,
+  /* BUNDLE_WQ: the radius R in a node's box margin a + b R (DESIGN.md "BVH cull": R bounds the ray
+   * origin's distance to every vertex below the node).  1 = the origin's distance to the farthest
+   * scene-box corner (once per ray); 2 = to the farthest corner of the node's own box (per node: more
+   * arithmetic, tighter boxes where margins are wide); default 0 = auto: 2 when
+   * HRT_SCENE_BVH_MARGIN_MILLI > 100 (cave), else 1.  Results do not depend on it. */
+  HRT_OPT_WQ_NODE_RADIUS = 16,
   /* libhip_raytrace_debug.so only (tests): the value-th device allocation of the next hrt_set_scene
    * fails with HRT_ERR_OUT_OF_MEMORY (0 = off) */
   HRT_DEBUG_OPT_FAIL_ALLOC = 1001,
@@ -280,7 +286,9 @@ typedef enum hrt_scene_info {
   HRT_SCENE_BVH_SAH_MILLI = 6,  /* 1000 x the expected leaf triangle tests of a uniform random ray per
                                    entry (surface-area estimate): < ~30 for a useful hierarchy; large
                                    overlapping triangles (a soup) give ~500, and auto then culls instead */
-  HRT_NUM_SCENE_INFO = 7
+  HRT_SCENE_BVH_MARGIN_MILLI = 7, /* 1000 x the mean over nodes of the box margin at R = the scene box's
+                                     diagonal / the box's largest extent (island 26, cave 197) */
+  HRT_NUM_SCENE_INFO = 8
 } hrt_scene_info;
 
 uint32_t hrt_abi_version(void);

@@ -155,6 +155,43 @@ def test_wq_pairs_bit_exact(scene, split, cap, width):
     ctx.close()
 
 
+@pytest.mark.parametrize("radius", [1, 2])
+@pytest.mark.parametrize("cap", [0, 128])
+@pytest.mark.parametrize("scene", ["island", "cave", "box", "ties"])
+def test_wq_node_radius_bit_exact(scene, cap, radius):
+    """HRT_OPT_WQ_NODE_RADIUS: node box margins a + b R with R the origin's distance to the farthest
+    scene-box corner (1) or to the farthest corner of each member's own box (2) -- both only ever keep
+    a node the reference could need; frames and counters stay the oracle's (cap 128: the stackless
+    fallback too)."""
+    if scene == "ties":
+        case = _tie_soup()
+    else:
+        case = SceneCase(scene, (64, 48), 2, 8)
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context(variant=9, options={_lib.OPT_WQ_NODE_RADIUS: radius, _lib.OPT_WQ_NODE_CAP: cap})
+    for _ in range(2):
+        ctx.reset_stats()
+        ctx.trace(case.push())
+        st = ctx.stats()
+        img = ctx.read(_lib.IMG_TRACE)
+        assert np.array_equal(img, ref), mismatch_report(img, ref)
+        assert (st.segments, st.tri_tests) == (seg, tt)
+    ctx.close()
+
+
+def test_wq_node_radius_auto_and_validation():
+    """Auto picks per-node radii from the scene's margin width (HRT_SCENE_BVH_MARGIN_MILLI > 100: cave,
+    not island); the option takes 0..2 only."""
+    for scene, wide in (("island", False), ("cave", True)):
+        case = SceneCase(scene, (16, 16), 1, 1)
+        ctx = case.context(variant=9)
+        assert (ctx.scene_info()["bvh_margin_milli"] > 100) == wide, ctx.scene_info()
+        for bad in (-1, 3):
+            with pytest.raises(Exception):
+                ctx.set_option(_lib.OPT_WQ_NODE_RADIUS, bad)
+        ctx.close()
+
+
 @pytest.mark.parametrize("leaf", [0, 4])
 @pytest.mark.parametrize("scene", ["island", "cave", "ties"])
 def test_wq_triangle_stack_bursts_tested_in_place(scene, leaf):
