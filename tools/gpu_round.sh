@@ -6,10 +6,12 @@ set -o pipefail
 TAG=${1:-r02}; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+if [ -z "$SKIP_TESTS" ]; then  # SKIP_TESTS=1: only the PMC passes, the bench line and the kernel trace
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 $OUT/gpu_tests.log; exit 1; }
 tail -2 $OUT/gpu_tests.log
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; cat $OUT/smoke.log; exit 1; }
 cat $OUT/smoke.log
+fi
 bash tools/pmc.sh $TAG/pmc "$@" > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $OUT/pmc.log; exit 1; }
 cp $OUT/pmc/pmc_traffic.json $OUT/pmc_traffic.json
 timeout -k 10 600 python3 bench.py --pmc-json $OUT/pmc_traffic.json "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
