@@ -2641,8 +2641,10 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
   *ran = variant;
   // bounce batch threshold, auto: the pair traversal's step cost scales with its rays, so BUNDLE_WQ
   // batches earlier (28 of 64 lanes); the cull kernels test every survivor for the whole wave (48)
-  // (profiles/r01q_sec_batch_sweep.jsonl, frames in 16-frame launches)
-  if (p.sec_batch == 0) p.sec_batch = variant == HRT_KERNEL_BUNDLE_WQ ? 28u : 48u;
+  // (profiles/r01q_sec_batch_sweep.jsonl, frames in 16-frame launches); 36 for the per-node-radius
+  // kernel, whose scenes bounce far more (cave 20 / 28 / 36 / 44 / 56: 7.43 / 7.38 / 7.31 / 7.32 /
+  // 7.45 ms; island stays best at 28: profiles/r02v_ab.txt)
+  if (p.sec_batch == 0) p.sec_batch = variant == HRT_KERNEL_BUNDLE_WQ ? (p.bvh_node_r ? 36u : 28u) : 48u;
   *block_out = variant == HRT_KERNEL_BRUTE_LDS ? 1024 : 256;
   const dim3 grid((p.pc.width + 15) / 16, (p.local_rows + 15) / 16, 1);
   switch (variant) {

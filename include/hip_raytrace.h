@@ -186,7 +186,7 @@ typedef enum hrt_option {
    * kernels' cull diagnostics (hrt_get_diagnostics) */
   HRT_OPT_COUNTERS = 2,
   /* bundle kernel: a wave runs its bounce (non-primary) segments once this many lanes wait for one,
-   * or when no lane has a primary segment left (1..64; default 0 = auto: 28 for BUNDLE_WQ, else 48;
+   * or when no lane has a primary segment left (1..64; default 0 = auto: 28 for BUNDLE_WQ (36 with per-node radii), else 48;
    * results do not depend on it) */
   HRT_OPT_SECONDARY_BATCH = 3,
   /* BUNDLE_BVH / BUNDLE_WQ: triangles per leaf of the hierarchy the next hrt_set_scene builds (1..16;
