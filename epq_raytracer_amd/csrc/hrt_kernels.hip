@@ -2450,7 +2450,8 @@ __device__ __forceinline__ float math_check_value(uint32_t& st, bool wide) {
 // sqrt on u01(k) and on -2 log(u01(k)), and spec_sincos_angle against spec_sincos on the two angle
 // forms of raytracing.glsl (u * 2 * pi and 6.2831852 * u); and adjust_dir's Lambertian shortcut
 // premise: a normal_dist radius sqrt(-2 log u) is finite and nonzero iff u is neither 0 nor 1, and the
-// cosine of 6.2831852 u is never 0 (and spec_log_u01 equals spec_log on every u01 value).
+// cosine of 6.2831852 u is never 0 (and spec_log_u01 equals spec_log on every u01 value); and
+// rcp_core's reciprocal is correctly rounded on div_core's range (k read as a float).
 // out[0..2]: violations of each.
 __global__ __launch_bounds__(256) void math_check_rng(uint32_t base, unsigned long long* out) {
   const uint32_t k = base + blockIdx.x * 256u + threadIdx.x;
@@ -2472,7 +2473,11 @@ __global__ __launch_bounds__(256) void math_check_rng(uint32_t base, unsigned lo
   const bool bad_log = fbits(spec_log_u01(u)) != fbits(spec_log(u));
   if (bad_sqrt) atomicAdd(&out[0], 1ull);
   if (bad_sc) atomicAdd(&out[1], 1ull);
-  if (bad_fast || bad_log) atomicAdd(&out[2], 1ull);
+  // rcp_core(b) = RN(1/b) for every float b in [2^-40, 2^40] (k read as a float), the premise of
+  // div_core's one correction
+  const float bk = bitsf(k);
+  const bool bad_rcp = bk >= 0x1p-40f && bk <= 0x1p40f && fbits(rcp_core(bk)) != fbits(1.0f / bk);
+  if (bad_fast || bad_log || bad_rcp) atomicAdd(&out[2], 1ull);
 }
 __global__ __launch_bounds__(256) void math_check(uint32_t n, uint32_t seed, unsigned long long* out) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;

@@ -60,10 +60,21 @@ __device__ __forceinline__ float rcp_core(float den) {  // the refined reciproca
   const float y0 = __builtin_amdgcn_rcpf(den);
   return __builtin_fmaf(__builtin_fmaf(-den, y0, 1.0f), y0, y0);
 }
+#ifndef HRT_DIV_MARKSTEIN
+#define HRT_DIV_MARKSTEIN 1
+#endif
 __device__ __forceinline__ float div_core(float num, float den, float y) {
   const float q = num * y;
   const float q1 = __builtin_fmaf(__builtin_fmaf(-den, q, num), y, q);
+#if HRT_DIV_MARKSTEIN
+  // rcp_core is RN(1/den) on the whole range (every float in [2^-40, 2^40], checked on the device:
+  // hrt_debug_math_check_rng), so q = RN(num y) is within 1 ulp of num / den and Markstein's theorem
+  // makes the first correction q1 = RN(q + (num - den q) y) the correctly rounded quotient (the
+  // residual is exact by the fma); the compiler's sequence's second correction changes nothing
+  return q1;
+#else
   return __builtin_fmaf(__builtin_fmaf(-den, q1, num), y, q1);
+#endif
 }
 // a / s for s > 0, correctly rounded (the shared-reciprocal path when every lane value is in range)
 __device__ __forceinline__ f3 div3(f3 a, float s) {
