@@ -46,7 +46,9 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
 // 1/den or quotient, num exponent > 23) and V_DIV_FIXUP_F32 passes the finite nonzero quotient
 // through, and where the sqrt input needs no pre-scale and is not special (x in [2^-96, 2^80]), the
 // sequences below ARE the compiler's instructions minus those identities -- the same bits -- and the
-// reciprocal of a common denominator is shared by the three components of a vector.
+// reciprocal of a common denominator is shared by the three components of a vector.  (Since r02v the
+// division also stops after q1: y is then already RN(1/den), so q1 is the correctly rounded quotient
+// by Markstein's theorem and the last correction never changes it; see div_core.)
 // tests/test_gpu_boundary.py::test_fast_division_and_sqrt_match_ieee checks them on the device.
 __device__ __forceinline__ float sqrt_core(float x) {  // x in [2^-96, 2^80]
   const float s = __builtin_amdgcn_sqrtf(x);
