@@ -58,8 +58,22 @@ def test_rccl_is_not_a_load_time_dependency():
 def test_code_object_targets_gfx950():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob  # the fat binary carries a gfx950 code object
-    for k in (b"trace_literal", b"trace_brute", b"trace_brute_lds", b"trace_bundle", b"trace_bundle_cull", b"trace_bundle_bvh", b"trace_bundle_cull_lds", b"trace_bundle_bvh_lds", b"camera_lists"):
+    for k in (b"trace_literal", b"trace_brute", b"trace_brute_lds", b"trace_bundle", b"trace_bundle_cull", b"trace_bundle_bvh", b"trace_bundle_cull_lds", b"trace_bundle_bvh_lds", b"camera_lists",
+              b"trace_bundle_wq", b"trace_bundle_wq_nr"):
         assert k in blob, k
+
+
+def test_node_radius_kernel_symbol():
+    """bench.py names the kernel its PMC record must match: BUNDLE_WQ runs trace_bundle_wq_nr when the
+    scene's margins are wide (HRT_SCENE_BVH_MARGIN_MILLI > 100) or HRT_OPT_WQ_NODE_RADIUS = 2."""
+    assert not _lib.wq_node_radius({"bvh_margin_milli": 26})
+    assert _lib.wq_node_radius({"bvh_margin_milli": 197})
+    assert _lib.wq_node_radius({"bvh_margin_milli": 26}, option=2)
+    assert not _lib.wq_node_radius({"bvh_margin_milli": 197}, option=1)
+    assert _lib.kernel_symbol(9, 1024) == "void hrt::trace_bundle_wq<false>(hrt::TraceParams)"
+    assert _lib.kernel_symbol(9, 1024, node_r=True) == "void hrt::trace_bundle_wq_nr<false>(hrt::TraceParams)"
+    assert _lib.kernel_symbol(7, 512, node_r=True) == "void hrt::trace_bundle_cull_lds<512, false>(hrt::TraceParams)"
+    assert "bvh_margin_milli" in _lib.SCENE_INFO_NAMES
 
 
 def test_record_layouts_match_std430():
