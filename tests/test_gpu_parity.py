@@ -179,6 +179,25 @@ def test_wq_node_radius_bit_exact(scene, cap, radius):
     ctx.close()
 
 
+@pytest.mark.parametrize("scene", ["island", "cave"])
+def test_wq_node_radius_full_frame_equal(scene):
+    """Both node-radius kernels over a whole 1080p frame (4 spp, 8 bounces, a 3-frame hrt_compute_n
+    launch): the same trace image, accumulator and counters."""
+    case = SceneCase(scene, (1920, 1080), 4, 8)
+    out = []
+    for radius in (1, 2):
+        ctx = case.context(variant=9, options={_lib.OPT_WQ_NODE_RADIUS: radius})
+        ctx.reset_stats()
+        ctx.compute_n(case.push(), 3)
+        st = ctx.stats()
+        out.append((ctx.read(_lib.IMG_TRACE), ctx.read(_lib.IMG_ACCUM), st.segments, st.tri_tests, st.last_kernel))
+        ctx.close()
+    (t1, a1, s1, x1, k1), (t2, a2, s2, x2, k2) = out
+    assert k1 == k2 == 9
+    assert np.array_equal(t1, t2) and np.array_equal(a1, a2), mismatch_report(t2, t1)
+    assert (s1, x1) == (s2, x2)
+
+
 def test_wq_node_radius_auto_and_validation():
     """Auto picks per-node radii from the scene's margin width (HRT_SCENE_BVH_MARGIN_MILLI > 100: cave,
     not island); the option takes 0..2 only."""
