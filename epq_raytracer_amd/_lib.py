@@ -116,7 +116,7 @@ SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh
 # Every symbol include/*.h declares (tests/test_abi.py checks the export table against this).
 EXPORTED_SYMBOLS = (
     "hrt_abi_version", "hrt_build_id", "hrt_debug_build", "hrt_debug_check_guards", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate", "hrt_compute_n",
-    "hrt_read_image", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
+    "hrt_read_image", "hrt_load_accumulator", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
     "hrt_get_diagnostics", "hrt_get_tile_profile", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
     "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory", "hrt_debug_math_check", "hrt_debug_math_check_rng",
     "hrt_stream", "hrt_last_error", "hrt_comm_unique_id", "hrt_comm_init", "hrt_comm_init_all", "hrt_comm_info",
@@ -165,6 +165,7 @@ def load(debug: bool = False) -> ctypes.CDLL:
         "hrt_accumulate": (c_int32, [P, c_uint32]),
         "hrt_compute_n": (c_int32, [P, POINTER(PushConstants), c_uint32]),
         "hrt_read_image": (c_int32, [P, c_uint32, c_uint32, P, c_size_t]),
+        "hrt_load_accumulator": (c_int32, [P, c_uint32, P, c_size_t]),
         "hrt_get_layout": (c_int32, [P, POINTER(Layout)]),
         "hrt_synchronize": (c_int32, [P]),
         "hrt_get_stats": (c_int32, [P, POINTER(Stats)]),

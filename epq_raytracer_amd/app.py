@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from typing import Callable, Optional
 
+import numpy as np
+
 from . import _lib
 from .pipeline import DiffusePipeline, HrtContext, Image, RayTracePipeline, RayTracerSettings
 from .scene import Camera
@@ -38,6 +40,27 @@ class RayTracingApp:
             render(diffuse.image())                             # :131-136
         self.pipeline = (raytrace, diffuse, render)
         self.frame += 1                                         # :139
+
+    def checkpoint(self, path: str) -> None:
+        """Save the progressive render's state (SURVEY.md §5 checkpoint / resume, not a reference
+        feature): the accumulated image in the context's own format and the frame counter."""
+        ctx = self.context
+        fmt = _lib.FMT_RGBA8 if ctx.mode == _lib.MODE_RGBA8 else _lib.FMT_RGBA32F
+        np.savez(path, accum=ctx.read(_lib.IMG_ACCUM, fmt), frame=np.uint64(self.frame), mode=np.uint32(ctx.mode),
+                 size=np.array([ctx.width, ctx.height, ctx.local_rows, ctx.row_tile, ctx.part_index, ctx.part_count],
+                               np.uint32))
+
+    def resume(self, path: str) -> None:
+        """Continue a checkpointed render on an open app of the same size, mode and partition: the next
+        frame traces with rng_offset = the saved frame counter, so the result equals an uninterrupted run."""
+        ctx = self.context
+        with np.load(path, allow_pickle=False) as z:
+            size = [int(v) for v in z["size"]]
+            if int(z["mode"]) != ctx.mode or size != [ctx.width, ctx.height, ctx.local_rows, ctx.row_tile,
+                                                       ctx.part_index, ctx.part_count]:
+                raise ValueError("checkpoint of another image size, mode or partition")
+            ctx.load_accumulator(z["accum"])
+            self.frame = int(z["frame"])
 
     def close(self) -> None:
         if self.context is not None:

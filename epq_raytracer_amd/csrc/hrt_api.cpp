@@ -826,6 +826,26 @@ extern "C" hrt_status hrt_read_image(hrt_context* ctx, uint32_t image_id, uint32
   return image_id == HRT_IMG_TRACE ? hrt::release_lane(ctx, ctx->cur_lane) : HRT_OK;
 }
 
+// Checkpoint / resume: the accumulator is the whole state of a progressive render
+// besides the frame counter (frame k traces with rng_offset = k), so restoring the bytes
+// hrt_read_image(HRT_IMG_ACCUM) returned -- in the context's own format, no conversion -- and
+// continuing with the saved frame number renders exactly what an uninterrupted run would.
+extern "C" hrt_status hrt_load_accumulator(hrt_context* ctx, uint32_t fmt, const void* src, size_t bytes) {
+  if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
+  const uint32_t native = ctx->accum8 ? HRT_FMT_RGBA8 : HRT_FMT_RGBA32F;
+  if (fmt != native)
+    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_load_accumulator: format must be the context's own (no conversion)");
+  if (!src) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_load_accumulator: null source");
+  const size_t need = ctx->npix() * (fmt == HRT_FMT_RGBA8 ? 4 : 16);
+  if (bytes != need) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_load_accumulator: size differs from the local image");
+  hrt_status st = bind(ctx);
+  if (st != HRT_OK) return st;
+  if ((st = sync_all(ctx)) != HRT_OK) return st;  // no accumulate in flight
+  void* dst = ctx->accum8 ? (void*)ctx->accum8 : (void*)ctx->accum32;
+  HRT_HIP(ctx, hipMemcpy(dst, src, need, hipMemcpyDefault));  // host or device source
+  return HRT_OK;
+}
+
 namespace hrt {
 hrt_status copy_frame_out(hrt_context* ctx, const void* src, size_t npix, uint32_t fmt, void* dst, void* scratch) {
   return copy_out(ctx, src, npix, fmt, dst, scratch);

@@ -209,6 +209,13 @@ class HrtContext:
         self._check(self.lib.hrt_read_image(self.handle, image_id, fmt, _lib.ptr(out), out.nbytes), "hrt_read_image")
         return out
 
+    def load_accumulator(self, img: np.ndarray):
+        """Checkpoint / resume: restore the accumulated image from an earlier read(IMG_ACCUM) in the
+        context's own format (hrt_load_accumulator)."""
+        fmt = _lib.FMT_RGBA8 if self.mode == _lib.MODE_RGBA8 else _lib.FMT_RGBA32F
+        img = np.ascontiguousarray(img)
+        self._check(self.lib.hrt_load_accumulator(self.handle, fmt, _lib.ptr(img), img.nbytes), "hrt_load_accumulator")
+
     def read_into(self, image_id: int, fmt: int, dst_ptr: int, nbytes: int):
         """Copy into caller memory (host or device pointer, e.g. a torch tensor's data_ptr())."""
         self._check(self.lib.hrt_read_image(self.handle, image_id, fmt, ctypes.c_void_p(dst_ptr), nbytes),

@@ -337,6 +337,13 @@ hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* pc, uint32_
  *    hrt_comm_init_all: any context of the group may call it alone; the frame lands in dst. */
 hrt_status hrt_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes);
 
+/* Checkpoint / resume (new): overwrite this context's local rows of the accumulated
+ * image with bytes an earlier hrt_read_image(HRT_IMG_ACCUM, fmt) returned, in the context's own format
+ * (HRT_FMT_RGBA8 for HRT_MODE_RGBA8, HRT_FMT_RGBA32F for HRT_MODE_RGBA32F; bytes = local_rows * width
+ * * 4 or 16).  Continuing with frame numbers from the saved count reproduces an uninterrupted render
+ * byte for byte.  src may be host or device memory. */
+hrt_status hrt_load_accumulator(hrt_context* ctx, uint32_t fmt, const void* src, size_t bytes);
+
 /* ---- multi-GPU framebuffer gather (RCCL is loaded on first use) ------------------- */
 #define HRT_COMM_ID_BYTES 128 /* == sizeof(ncclUniqueId) */
 typedef enum hrt_comm_transport {

@@ -199,6 +199,10 @@ class Context {
     return s;
   }
   void synchronize() { check(hrt_synchronize(get()), "hrt_synchronize", get()); }
+  // checkpoint / resume: restore the accumulator from bytes read_rgba8(HRT_IMG_ACCUM) returned
+  void load_accumulator_rgba8(const std::vector<uint8_t>& img) {
+    check(hrt_load_accumulator(get(), HRT_FMT_RGBA8, img.data(), img.size()), "hrt_load_accumulator", get());
+  }
   // the context's local rows of an image: rgba8 bytes (local_rows x width x 4)
   std::vector<uint8_t> read_rgba8(hrt_image_id image) const {
     std::vector<uint8_t> out((size_t)layout_.local_rows * layout_.width * 4);
