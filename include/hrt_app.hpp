@@ -300,6 +300,7 @@ class RayTracePipeline {  // src/raytrace_pipeline.rs:31-266
     check(hrt_trace(ctx_->get(), &pc), "hrt_trace", ctx_->get());
   }
   Context& context() const { return *ctx_; }
+  std::array<uint32_t, 2> image_size() const { return size_; }
 
  private:
   Context* ctx_;
@@ -314,6 +315,7 @@ class DiffusePipeline {  // src/diffuse.rs:22-136 (image_combiner.glsl)
  public:
   DiffusePipeline(Context& ctx, std::array<uint32_t, 2> image_size) : ctx_(&ctx), size_(image_size) {}
   Image image() const { return Image{ctx_, HRT_IMG_ACCUM}; }  // :69
+  std::array<uint32_t, 2> image_size() const { return size_; }
   void next_frame(uint32_t frame_num, const Image& next_image) {  // :73-136
     if (next_image.ctx != ctx_ || next_image.id != HRT_IMG_TRACE)
       throw HrtError(HRT_ERR_INVALID_ARGUMENT, "next_frame: next_image must be the trace image of the same context");
