@@ -14,6 +14,12 @@ measured after the timed steps.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+Without a launcher (WORLD_SIZE unset) and --gpus N > 1, this process starts the N rank processes itself
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1) before anything in it touches a GPU, and
+exits with the first failing rank's status; under a launcher --gpus must equal WORLD_SIZE.  For N > 1
+--verify is on by default: rank 0 re-renders the frames on one full-frame context and the line's
+gather_check says whether the gathered framebuffer is byte-identical to it.
+
 A "ray" is one segment = one world_hit call (assets/raytracing.glsl:317), counted exactly on the
 device.  value = segments of all ranks / max-over-ranks wall time of the K timed steps.
 Prints ONE JSON line on rank 0 (fields: DESIGN.md "Measurement").
@@ -23,6 +29,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -53,8 +61,9 @@ def parse():
     ap.add_argument("--frames-per-launch", type=int, default=64,
                     help="> 1: steps run as hrt_compute_n (compute_n_then_render) with up to this many frames per "
                          "trace launch; 1: one trace + accumulate (+ gather) dispatch per step (compute_then_render)")
-    ap.add_argument("--verify", action="store_true",
-                    help="N>1: rank 0 re-renders all frames on one full-frame context and compares the gathered frame")
+    ap.add_argument("--verify", action=argparse.BooleanOptionalAction, default=None,
+                    help="N>1 (default on): rank 0 re-renders all frames on one full-frame context and compares "
+                         "the gathered frame byte for byte (gather_check)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = the library's RCCL gather over xGMI (default); gloo = torch all-gather of the "
                          "local blocks through the host (rehearsal with several ranks on one GPU)")
@@ -67,19 +76,84 @@ def parse():
     return ap.parse_args()
 
 
+def resolve_launch(gpus: int, env) -> tuple:
+    """("spawn", N): no launcher (WORLD_SIZE unset) and N > 1 -- this process starts the N ranks;
+    ("rank", world): run as one rank of world.  A --gpus that contradicts the launcher's WORLD_SIZE is
+    an error, never a silent single-rank line."""
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in env:
+        return ("spawn", gpus) if gpus > 1 else ("rank", 1)
+    world = int(env["WORLD_SIZE"])
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+    return ("rank", world)
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, cmd=None, poll_s: float = 0.1) -> int:
+    """Start n rank processes (cmd + argv, default this script) with the torch.distributed.run
+    environment, one per GPU, and wait for them.  Returns 0, or the first failing rank's exit status
+    after terminating the others (by their own PIDs).  Nothing here touches a GPU: the ranks are fresh
+    processes, not forks of an initialised runtime."""
+    port = free_port()
+    base = cmd or [sys.executable, os.path.abspath(__file__)]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen(base + list(argv), env=env))
+    status = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]  # (every rank polled: no short-circuit)
+            if all(c is not None for c in codes):
+                break
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                status = bad[0]
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if status == 0:
+        status = next((p.returncode for p in procs if p.returncode != 0), 0)
+    return status
+
+
 def main():
     args = parse()
+    how, world = resolve_launch(args.gpus, os.environ)
+    if how == "spawn":
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.verify is None:
+        args.verify = world > 1
 
     import torch
     import torch.distributed as dist
 
     dist_on = world > 1
-    ndev = max(torch.cuda.device_count(), 1)
-    device = local_rank % ndev  # one rank per GPU; ranks > GPUs only for gloo rehearsals
     gloo = args.dist_backend == "gloo"
+    ndev = torch.cuda.device_count()  # (counts devices without initialising the runtime)
+    if dist_on and not gloo and world > ndev:
+        raise SystemExit(f"bench.py: --gpus {world} with the RCCL gather needs {world} GPUs, {ndev} visible "
+                         "(--dist-backend gloo rehearses several ranks on one GPU)")
+    device = local_rank % max(ndev, 1)  # one rank per GPU; ranks > GPUs only for gloo rehearsals
     if dist_on:
         torch.cuda.set_device(device)
         if gloo:
@@ -229,6 +303,8 @@ def main():
                        "parallelism": (f"row-tiles{world}x{args.row_tile} (" +
                                        ("RCCL ncclGather behind hrt_read_image" if lib_gather else "gloo all-gather")
                                        + ")" if dist_on else "single-gpu"),
+                       "launcher": ("bench.py --gpus (own rank processes)" if os.environ.get("BENCH_SPAWNED")
+                                    else "torch.distributed.run" if dist_on else "single process"),
                        "kernel_variant": _lib.KERNEL_NAMES[args.variant]},
             "segments_per_step": segs_all // args.steps,
             "tri_tests_per_step": tests_all // args.steps,

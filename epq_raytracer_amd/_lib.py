@@ -66,15 +66,19 @@ class Stats(ctypes.Structure):
                 ("last_kernel", c_uint32), ("last_block", c_uint32)]
 
 
+ABI_VERSION = 2  # HRT_ABI_VERSION this binding's signatures describe
 HRT_OK = 0
 STATUS_NAMES = {0: "HRT_OK", 1: "HRT_ERR_INVALID_ARGUMENT", 2: "HRT_ERR_NO_DEVICE", 3: "HRT_ERR_OUT_OF_MEMORY",
-                4: "HRT_ERR_NO_SCENE", 5: "HRT_ERR_HIP", 6: "HRT_ERR_IO"}
+                4: "HRT_ERR_NO_SCENE", 5: "HRT_ERR_HIP", 6: "HRT_ERR_IO", 7: "HRT_ERR_COMM"}
+ERR_COMM = 7
 MODE_RGBA8, MODE_RGBA32F = 0, 1
 IMG_TRACE, IMG_ACCUM = 0, 1
+IMG_LOCAL = 0x100  # flag: this context's local rows, never the collective gather
 FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
 OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP, OPT_WQ_NODE_CAP, OPT_PROBE = 5, 6, 7, 8, 9, 10, 11
 OPT_FRAMES_PER_LAUNCH, OPT_OVERLAP, OPT_BUSY_SPLIT, OPT_BVH_WIDTH, OPT_WQ_NODE_RADIUS = 12, 13, 14, 15, 16
+OPT_COMM_TIMEOUT_MS = 17
 DEBUG_OPT_FAIL_ALLOC = 1001  # libhip_raytrace_debug.so only
 DEBUG_OPT_WQ_TRI_CAP = 1002  # libhip_raytrace_debug.so only
 COMM_ID_BYTES = 128
@@ -148,6 +152,11 @@ def load(debug: bool = False) -> ctypes.CDLL:
         raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                            " or `make -C epq_raytracer_amd/csrc` (no CPU fallback exists)")
     lib = ctypes.CDLL(path)
+    lib.hrt_abi_version.restype = c_uint32
+    lib.hrt_abi_version.argtypes = []
+    if lib.hrt_abi_version() != ABI_VERSION:  # the signatures below would bind shifted arguments
+        raise RuntimeError(f"{path} implements HRT_ABI_VERSION {lib.hrt_abi_version()}, this binding "
+                           f"{ABI_VERSION}: rebuild it (make -C epq_raytracer_amd/csrc)")
     P = c_void_p
     sig = {
         "hrt_abi_version": (c_uint32, []),

@@ -389,10 +389,23 @@ struct SceneAlloc {
 // 359,371-372, stage through host-visible buffers the same way).
 hrt_status stage_upload(hrt_context* ctx, void* dst, const void* src, size_t bytes) {
   auto& s = ctx->staging;
-  if (!s.buf[0]) {
+  if (!s.chunk) {  // both chunks and events into locals; published only when all four exist
+    void* buf[2] = {};
+    hipEvent_t ev[2] = {};
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 2 && e == hipSuccess; ++i)
+      if ((e = hipHostMalloc(&buf[i], kStagingChunk, hipHostMallocDefault)) == hipSuccess)
+        e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+      for (int i = 0; i < 2; ++i) {
+        if (buf[i]) (void)hipHostFree(buf[i]);
+        if (ev[i]) (void)hipEventDestroy(ev[i]);
+      }
+      return hip_fail(ctx, e, "hrt_set_scene: pinned staging");
+    }
     for (int i = 0; i < 2; ++i) {
-      HRT_HIP(ctx, hipHostMalloc(&s.buf[i], kStagingChunk, hipHostMallocDefault));
-      HRT_HIP(ctx, hipEventCreateWithFlags(&s.ev[i], hipEventDisableTiming));
+      s.buf[i] = buf[i];
+      s.ev[i] = ev[i];
       s.used[i] = false;
     }
     s.chunk = kStagingChunk;
@@ -809,11 +822,16 @@ hrt_status copy_out(hrt_context* ctx, const void* src, size_t npix, uint32_t fmt
 
 extern "C" hrt_status hrt_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes) {
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
+  const bool local = (image_id & HRT_IMG_LOCAL) != 0;
+  image_id &= ~(uint32_t)HRT_IMG_LOCAL;
+  hrt_status arg = HRT_OK;
   if (image_id != HRT_IMG_TRACE && image_id != HRT_IMG_ACCUM)
-    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown image id");
-  if (fmt != HRT_FMT_RGBA8 && fmt != HRT_FMT_RGBA32F)
-    return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown format");
-  if (ctx->comm) return hrt::comm_read_image(ctx, image_id, fmt, dst, bytes);  // the framebuffer gather
+    arg = fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown image id");
+  else if (fmt != HRT_FMT_RGBA8 && fmt != HRT_FMT_RGBA32F)
+    arg = fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: unknown format");
+  // the framebuffer gather: a collective, so a bad argument is agreed on by every rank, not returned here
+  if (ctx->comm && !local) return hrt::comm_read_image(ctx, image_id, fmt, dst, bytes, arg);
+  if (arg != HRT_OK) return arg;
   if (!dst) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_read_image: null destination");
   const size_t np = ctx->npix();
   if (bytes < np * (fmt == HRT_FMT_RGBA8 ? 4 : 16))
@@ -842,7 +860,9 @@ extern "C" hrt_status hrt_load_accumulator(hrt_context* ctx, uint32_t fmt, const
   if (st != HRT_OK) return st;
   if ((st = sync_all(ctx)) != HRT_OK) return st;  // no accumulate in flight
   void* dst = ctx->accum8 ? (void*)ctx->accum8 : (void*)ctx->accum32;
-  HRT_HIP(ctx, hipMemcpy(dst, src, need, hipMemcpyDefault));  // host or device source
+  // on the context stream (non-blocking w.r.t. the null stream): the next hrt_accumulate follows it
+  HRT_HIP(ctx, hipMemcpyAsync(dst, src, need, hipMemcpyDefault, ctx->stream));  // host or device source
+  HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return HRT_OK;
 }
 
@@ -1145,6 +1165,11 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
     case HRT_OPT_WQ_NODE_RADIUS:
       if (value < 0 || value > 2) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "wq node radius must be 0 (auto), 1 or 2");
       ctx->wq_node_radius = (uint32_t)value;
+      return HRT_OK;
+    case HRT_OPT_COMM_TIMEOUT_MS:
+      if (value < 0 || value > 0xFFFFFFFFll)
+        return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "comm timeout must be in [0, 2^32) ms (0 = wait forever)");
+      ctx->comm_timeout_ms = (uint32_t)value;
       return HRT_OK;
     case HRT_OPT_BVH_LEAF_SIZE:
       if (value < 0 || value > hrt::kBvhMaxLeafCount)

@@ -154,6 +154,7 @@ struct hrt_context {
   std::vector<Guard> guards;  // debug build: guarded device allocations (hrt_debug_check_guards)
   hrt::Staging staging;
   hrt::Comm* comm = nullptr;  // hrt_comm_init / hrt_comm_init_all
+  uint32_t comm_timeout_ms = 120000;  // HRT_OPT_COMM_TIMEOUT_MS (0: wait forever)
 
   std::string err;
 
@@ -176,8 +177,10 @@ hrt_status release_lane(hrt_context* ctx, int l);  // lane l's buffers are free 
 const void* local_image(hrt_context* ctx, uint32_t image_id);
 // dst <- npix pixels at src (context format) converted to fmt via scratch, ordered on ctx->stream; blocking.
 hrt_status copy_frame_out(hrt_context* ctx, const void* src, size_t npix, uint32_t fmt, void* dst, void* scratch);
-// hrt_read_image on a context with a communicator (hrt_comm.cpp).
-hrt_status comm_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes);
+// hrt_read_image on a context with a communicator (hrt_comm.cpp); arg = the caller's own argument
+// check, agreed on by every rank of a process communicator before any of them gathers.
+hrt_status comm_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes,
+                           hrt_status arg);
 
 }  // namespace hrt
 

@@ -203,10 +203,13 @@ class HrtContext:
         self._check(self.lib.hrt_reset_stats(self.handle), "hrt_reset_stats")
 
     def read(self, image_id: int, fmt: int = _lib.FMT_RGBA8) -> np.ndarray:
-        """Local rows of an image: uint8 (local_rows, W, 4) or float32 (local_rows, W, 4)."""
+        """Local rows of an image: uint8 (local_rows, W, 4) or float32 (local_rows, W, 4) -- this
+        context's own rows even when it is joined to a communicator (HRT_IMG_LOCAL: never the
+        collective gather; read_frame is the gathered frame)."""
         dt = np.uint8 if fmt == _lib.FMT_RGBA8 else np.float32
         out = np.empty((self.local_rows, self.width, 4), dtype=dt)
-        self._check(self.lib.hrt_read_image(self.handle, image_id, fmt, _lib.ptr(out), out.nbytes), "hrt_read_image")
+        self._check(self.lib.hrt_read_image(self.handle, image_id | _lib.IMG_LOCAL, fmt, _lib.ptr(out), out.nbytes),
+                    "hrt_read_image")
         return out
 
     def load_accumulator(self, img: np.ndarray):
@@ -283,8 +286,14 @@ class Image:
     def __init__(self, ctx: HrtContext, image_id: int):
         self.ctx, self.image_id = ctx, image_id
 
-    def read(self, fmt: int = _lib.FMT_RGBA8) -> np.ndarray:
-        return self.ctx.read(self.image_id, fmt)
+    def read(self, fmt: int = _lib.FMT_RGBA8) -> Optional[np.ndarray]:
+        """What the presenter gets.  Without a communicator: the context's rows.  On a context joined to
+        one (hrt_comm_init): the gathered FULL frame -- a collective every rank must call; ranks other
+        than 0 get None.  On a group (hrt_comm_init_all): the full frame."""
+        rank, _, transport = self.ctx.comm_info()
+        if transport == _lib.COMM_NONE:
+            return self.ctx.read(self.image_id, fmt)
+        return self.ctx.read_frame(self.image_id, fmt, root=transport != _lib.COMM_RCCL or rank == 0)
 
 
 # ---- pipelines ---------------------------------------------------------------------------------

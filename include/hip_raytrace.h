@@ -39,7 +39,9 @@
 extern "C" {
 #endif
 
-#define HRT_ABI_VERSION 1u
+/* 2 (r03): HRT_ERR_COMM, HRT_IMG_LOCAL, HRT_OPT_COMM_TIMEOUT_MS, collective error agreement;
+ * hrt_debug_bvh_wq_nodes' width parameter; HRT_NUM_DIAG / HRT_NUM_SCENE_INFO grown (r02). */
+#define HRT_ABI_VERSION 2u
 
 typedef enum hrt_status {
   HRT_OK = 0,
@@ -48,7 +50,10 @@ typedef enum hrt_status {
   HRT_ERR_OUT_OF_MEMORY = 3,
   HRT_ERR_NO_SCENE = 4,         /* hrt_trace before hrt_set_scene */
   HRT_ERR_HIP = 5,              /* a HIP runtime call failed; hrt_last_error has the text */
-  HRT_ERR_IO = 6                /* file not found / unparsable (host helpers) */
+  HRT_ERR_IO = 6,               /* file not found / unparsable (host helpers) */
+  HRT_ERR_COMM = 7              /* a collective (hrt_comm_init, hrt_read_image on a joined context) failed
+                                   on ANOTHER rank, timed out or was aborted; every rank of the call
+                                   returns an error and none is left blocked (hrt_comm.cpp) */
 } hrt_status;
 
 /* ---- std430 records (assets/raytracing.glsl:51-111) ---------------------------------------- */
@@ -114,7 +119,13 @@ typedef enum hrt_mode {
   HRT_MODE_RGBA32F = 1 /* fp32 images, same arithmetic without the per-frame 8-bit requantization */
 } hrt_mode;
 
-typedef enum hrt_image_id { HRT_IMG_TRACE = 0, HRT_IMG_ACCUM = 1 } hrt_image_id;
+typedef enum hrt_image_id {
+  HRT_IMG_TRACE = 0,
+  HRT_IMG_ACCUM = 1,
+  /* flag, OR-ed with one of the above: this context's LOCAL rows even when it is joined to a
+   * communicator -- not a collective (checkpoints of a partition, per-rank inspection) */
+  HRT_IMG_LOCAL = 0x100
+} hrt_image_id;
 typedef enum hrt_format { HRT_FMT_RGBA8 = 0, HRT_FMT_RGBA32F = 1 } hrt_format;
 
 typedef struct hrt_create_info {
@@ -241,6 +252,10 @@ typedef enum hrt_option {
    * arithmetic, tighter boxes where margins are wide); default 0 = auto: 2 when
    * HRT_SCENE_BVH_MARGIN_MILLI > 100 (cave), else 1.  Results do not depend on it. */
   HRT_OPT_WQ_NODE_RADIUS = 16,
+  /* hrt_comm_init / collective hrt_read_image: milliseconds a rank waits for its peers in the status
+   * agreement or the gather before it aborts the communicator (ncclCommAbort) and returns
+   * HRT_ERR_COMM (default 120000; 0 = wait forever).  Per context. */
+  HRT_OPT_COMM_TIMEOUT_MS = 17,
   /* libhip_raytrace_debug.so only (tests): the value-th device allocation of the next hrt_set_scene
    * fails with HRT_ERR_OUT_OF_MEMORY (0 = off) */
   HRT_DEBUG_OPT_FAIL_ALLOC = 1001,
@@ -330,10 +345,14 @@ hrt_status hrt_accumulate(hrt_context* ctx, uint32_t frame);
 hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* pc, uint32_t n);
 
 /* Copy an image (row-major, x 4 channels) into dst, host or device memory.  Blocking.
- *  - Without a communicator: this context's local rows (local_rows x width); bytes >= that in fmt.
+ *  - Without a communicator, or with image_id | HRT_IMG_LOCAL: this context's local rows
+ *    (local_rows x width); bytes >= that in fmt.
  *  - With one (hrt_comm_init / hrt_comm_init_all): the FULL frame (height x width), gathered from every
  *    part with one ncclGather to rank 0 and un-interleaved on rank 0's device.  hrt_comm_init: a
  *    collective -- every rank calls it; dst / bytes are used on rank 0 only (may be NULL elsewhere).
+ *    Every rank first agrees on the call's status: if any rank's arguments or local image are bad,
+ *    every rank returns an error (HRT_ERR_COMM on the others) and none enters the gather; a peer that
+ *    does not arrive within HRT_OPT_COMM_TIMEOUT_MS aborts the communicator (later calls: HRT_ERR_COMM).
  *    hrt_comm_init_all: any context of the group may call it alone; the frame lands in dst. */
 hrt_status hrt_read_image(hrt_context* ctx, uint32_t image_id, uint32_t fmt, void* dst, size_t bytes);
 
@@ -355,7 +374,10 @@ typedef enum hrt_comm_transport {
 /* A fresh RCCL unique id (ncclGetUniqueId) for hrt_comm_init; rank 0 creates it and shares the bytes. */
 hrt_status hrt_comm_unique_id(uint8_t id[HRT_COMM_ID_BYTES]);
 /* Joins ctx -- part `rank` of a `world`-way row-tile partition (hrt_create_info), or the whole image
- * when world == 1 -- to the communicator named by id.  Collective: blocks until all ranks joined. */
+ * when world == 1 -- to the communicator named by id.  Collective: blocks until all ranks joined.
+ * The root's buffers are allocated before the communicator is created, and the ranks agree on the
+ * outcome: a rank whose partition does not match or whose allocation failed makes every rank return
+ * an error with no communicator (a NULL id, rank >= world or a missing RCCL cannot join at all). */
 hrt_status hrt_comm_init(hrt_context* ctx, const uint8_t id[HRT_COMM_ID_BYTES], uint32_t rank, uint32_t world);
 /* One process driving every part: ctxs[i] must be part i of n (same size, mode, row tile). */
 hrt_status hrt_comm_init_all(hrt_context* const* ctxs, uint32_t n);

@@ -25,6 +25,7 @@
 
 #include <array>
 #include <cstdint>
+#include <cstring>
 #include <functional>
 #include <memory>
 #include <optional>
@@ -199,16 +200,23 @@ class Context {
     return s;
   }
   void synchronize() { check(hrt_synchronize(get()), "hrt_synchronize", get()); }
-  // checkpoint / resume: restore the accumulator from bytes read_rgba8(HRT_IMG_ACCUM) returned
+  // the context's own pixel format (rgba8 or rgba32f): what checkpoints hold
+  hrt_format native_format() const { return layout_.mode == HRT_MODE_RGBA8 ? HRT_FMT_RGBA8 : HRT_FMT_RGBA32F; }
+  // checkpoint / resume: restore the accumulator from bytes read(HRT_IMG_ACCUM, native_format()) returned
+  void load_accumulator(const std::vector<uint8_t>& img) {
+    check(hrt_load_accumulator(get(), native_format(), img.data(), img.size()), "hrt_load_accumulator", get());
+  }
   void load_accumulator_rgba8(const std::vector<uint8_t>& img) {
     check(hrt_load_accumulator(get(), HRT_FMT_RGBA8, img.data(), img.size()), "hrt_load_accumulator", get());
   }
-  // the context's local rows of an image: rgba8 bytes (local_rows x width x 4)
-  std::vector<uint8_t> read_rgba8(hrt_image_id image) const {
-    std::vector<uint8_t> out((size_t)layout_.local_rows * layout_.width * 4);
-    check(hrt_read_image(get(), image, HRT_FMT_RGBA8, out.data(), out.size()), "hrt_read_image", get());
+  // the context's local rows of an image in fmt (local_rows x width x 4 channels of 1 or 4 bytes); never
+  // the collective gather (HRT_IMG_LOCAL), also on a context joined to a communicator
+  std::vector<uint8_t> read(hrt_image_id image, hrt_format fmt) const {
+    std::vector<uint8_t> out((size_t)layout_.local_rows * layout_.width * (fmt == HRT_FMT_RGBA8 ? 4 : 16));
+    check(hrt_read_image(get(), (uint32_t)image | HRT_IMG_LOCAL, fmt, out.data(), out.size()), "hrt_read_image", get());
     return out;
   }
+  std::vector<uint8_t> read_rgba8(hrt_image_id image) const { return read(image, HRT_FMT_RGBA8); }
 
  private:
   struct Del {
@@ -347,6 +355,27 @@ class RayTracingApp {
   }
   bool is_open() const { return ctx_ != nullptr; }
   uint32_t frame() const { return frame_; }
+
+  // Checkpoint / resume (not a reference feature): the accumulator in the context's own
+  // format plus the frame counter are the whole state of a progressive render (frame k traces with
+  // rng_offset = k), so resuming on an open app of the same size and mode continues it byte for byte.
+  struct Checkpoint {
+    std::vector<uint8_t> accum;
+    uint32_t frame = 0;
+    hrt_layout layout{};
+  };
+  Checkpoint checkpoint() const {
+    require_open();
+    return Checkpoint{ctx_->read(HRT_IMG_ACCUM, ctx_->native_format()), frame_, ctx_->layout()};
+  }
+  void resume(const Checkpoint& c) {
+    require_open();
+    const hrt_layout& l = ctx_->layout();
+    if (std::memcmp(&l, &c.layout, sizeof l) != 0)
+      throw HrtError(HRT_ERR_INVALID_ARGUMENT, "RayTracingApp::resume: checkpoint of another size, mode or partition");
+    ctx_->load_accumulator(c.accum);
+    frame_ = c.frame;
+  }
   RayTracePipeline& raytrace() { return *raytrace_; }
   DiffusePipeline& diffuse() { return *diffuse_; }
   Context& context() { return *ctx_; }

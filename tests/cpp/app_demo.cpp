@@ -2,7 +2,10 @@
 // compute_n_then_render) written against include/hrt_app.hpp, the C++ mirror of its public surface.
 // tests/test_cpp_app.py renders the same scene through the Python mirror and compares the frames.
 //
-//   app_demo <out.bin> <width> <height> <spp> <bounces> <frames> <loop|batch> [obj path]
+//   app_demo <out.bin> <width> <height> <spp> <bounces> <frames> <loop|batch|resume|resume32> [obj path]
+//
+// resume / resume32 (rgba8 / rgba32f mode): frames / 2 frames through compute_n_then_render, a
+// checkpoint, a NEW app that resumes from it, the remaining frames through compute_then_render.
 //
 // Scene (fixed here, mirrored in tests/test_cpp_app.py::demo_settings): a ground sphere, a metal and
 // a light sphere, an invisible light, and a two-triangle quad with a custom material (plus every mesh
@@ -12,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 
 #include "hrt_app.hpp"
@@ -49,31 +53,48 @@ int main(int argc, char** argv) {
   const uint32_t spp = (uint32_t)std::atoi(argv[4]), bounces = (uint32_t)std::atoi(argv[5]);
   const uint32_t frames = (uint32_t)std::atoi(argv[6]);
   const bool batch = std::strcmp(argv[7], "batch") == 0;
+  const bool resume = std::strncmp(argv[7], "resume", 6) == 0;
+  const hrt_mode mode = std::strcmp(argv[7], "resume32") == 0 ? HRT_MODE_RGBA32F : HRT_MODE_RGBA8;
   try {
     epq::Camera cam;
     cam.position = {0.0f, 0.3f, 1.5f};
     cam.direction = {0.0f, -0.1f, -1.0f};
-    epq::RayTracingApp app(cam, demo_settings(spp, bounces, argc > 8 ? argv[8] : nullptr));
+    const epq::RayTracerSettings settings = demo_settings(spp, bounces, argc > 8 ? argv[8] : nullptr);
+    auto app = std::make_unique<epq::RayTracingApp>(cam, settings, -1, mode);
     uint32_t presented = 0;
-    app.open({w, h}, [&](const epq::Image&) { ++presented; });
+    app->open({w, h}, [&](const epq::Image&) { ++presented; });
+    uint64_t seg = 0, tt = 0;
     if (batch) {
-      epq::compute_n_then_render(app, frames);
+      epq::compute_n_then_render(*app, frames);
+    } else if (resume) {
+      epq::compute_n_then_render(*app, frames / 2);
+      const epq::RayTracingApp::Checkpoint ck = app->checkpoint();
+      const hrt_stats s1 = app->context().stats();
+      seg += s1.segments;
+      tt += s1.tri_tests;
+      app = std::make_unique<epq::RayTracingApp>(cam, settings, -1, mode);  // a restart
+      app->open({w, h});
+      app->resume(ck);
+      for (uint32_t k = frames / 2; k < frames; ++k) epq::compute_then_render(*app, 1.0f / 60.0f);
     } else {
-      for (uint32_t k = 0; k < frames; ++k) epq::compute_then_render(app, 1.0f / 60.0f);
+      for (uint32_t k = 0; k < frames; ++k) epq::compute_then_render(*app, 1.0f / 60.0f);
     }
-    const hrt_stats st = app.context().stats();
-    const std::vector<uint8_t> img = app.diffuse().image().read_rgba8();
+    epq::RayTracingApp& app_ = *app;
+    const hrt_stats st = app_.context().stats();
+    const std::vector<uint8_t> img = app_.diffuse().image().read_rgba8();
     FILE* f = std::fopen(argv[1], "wb");
     if (!f) return 3;
-    const uint64_t seg = st.segments, tt = st.tri_tests;
-    const uint32_t fr = app.frame();
+    seg += st.segments;
+    tt += st.tri_tests;
+    const uint32_t fr = app_.frame();
     std::fwrite(&seg, 8, 1, f);
     std::fwrite(&tt, 8, 1, f);
     std::fwrite(&fr, 4, 1, f);
     std::fwrite(img.data(), 1, img.size(), f);
     std::fclose(f);
     std::printf("app_demo: %ux%u %u spp %u bounces, %u frames (%s), %u presents, %llu segments\n", w, h, spp, bounces,
-                frames, batch ? "compute_n_then_render" : "compute_then_render", presented, (unsigned long long)seg);
+                frames, batch ? "compute_n_then_render" : resume ? "checkpoint + resume" : "compute_then_render", presented,
+                (unsigned long long)seg);
     return 0;
   } catch (const epq::HrtError& e) {
     std::fprintf(stderr, "app_demo: %s\n", e.what());

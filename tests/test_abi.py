@@ -33,7 +33,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_library_loads_and_reports_abi():
     lib = _lib.load()
-    assert lib.hrt_abi_version() == 1
+    assert lib.hrt_abi_version() == _lib.ABI_VERSION == 2
     assert lib.hrt_debug_build() == 0
     assert len(_lib.build_id()) == 16 and _lib.build_id() != "unknown"
 
@@ -41,7 +41,7 @@ def test_library_loads_and_reports_abi():
 def test_debug_library_is_the_same_abi():
     """libhip_raytrace_debug.so: the same exports, hrt_debug_build() == 1, the same device code."""
     dbg = _lib.load(debug=True)
-    assert dbg.hrt_debug_build() == 1 and dbg.hrt_abi_version() == 1
+    assert dbg.hrt_debug_build() == 1 and dbg.hrt_abi_version() == _lib.ABI_VERSION
     assert dbg.hrt_build_id().decode() == _lib.build_id()
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.DEBUG_LIB_PATH], capture_output=True, text=True,
                          check=True)

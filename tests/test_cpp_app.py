@@ -2,7 +2,11 @@
 reference's flow (RayTracingApp::open, compute_then_render / compute_n_then_render over
 RayTracePipeline + DiffusePipeline, src/raytracing_app.rs:74-227) in C++; the same scene through the
 Python mirror (epq_raytracer_amd.app) must give the same accumulated frame, counters and frame counter
-byte for byte.  Without a device the binary fails loudly (hrt_create -> HRT_ERR_NO_DEVICE)."""
+byte for byte, and -- so that a record-packing defect shared by both mirrors cannot pass (VERDICT r02
+weak #10) -- the rgba8 accumulator must equal the CPU oracle's trace + combiner over the same frames
+(records built by the host prep, src/objects.rs:14-47, src/materials.rs:13-94).  The resume modes
+checkpoint the C++ app half way, restart it and resume (RayTracingApp::checkpoint / resume).
+Without a device the binary fails loudly (hrt_create -> HRT_ERR_NO_DEVICE)."""
 import os
 import subprocess
 
@@ -10,7 +14,9 @@ import numpy as np
 import pytest
 
 import epq_raytracer_amd as E
+import pyoracle
 from epq_raytracer_amd import _lib
+from helpers import SceneCase
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DEMO = os.path.join(ROOT, "tests", "cpp", "app_demo")
@@ -68,10 +74,25 @@ def test_demo_builds_and_fails_loudly_without_a_device(tmp_path):
     assert "hrt_create" in r.stderr
 
 
+def oracle_accumulator(w, h, spp, bounces, frames, obj_path, cam):
+    """The oracle's rgba8 accumulator after the reference's frame sequence (clear, then trace k +
+    combine(k), k = 1..frames) on the demo scene's records."""
+    case = SceneCase(None, (w, h), spp, bounces, settings=demo_settings(spp, bounces, obj_path), camera=cam)
+    acc = np.zeros((h, w, 4), np.uint8)
+    segs = tests = 0
+    pyoracle.accumulate_rgba8(0, acc, acc.copy())
+    for k in range(1, frames + 1):
+        img, _, s, t = case.oracle(rng_offset=k)
+        pyoracle.accumulate_rgba8(k, acc, img)
+        segs, tests = segs + s, tests + t
+    return acc, segs, tests
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,obj", [("loop", False), ("batch", False), ("loop", True)])
+@pytest.mark.parametrize("mode,obj", [("loop", False), ("batch", False), ("loop", True), ("resume", False),
+                                      ("resume32", True)])
 def test_cpp_app_matches_python_mirror(tmp_path, mode, obj):
-    w, h, spp, bounces, frames = 96, 64, 4, 5, 3
+    w, h, spp, bounces, frames = 96, 64, 4, 5, 3 if not mode.startswith("resume") else 5
     obj_path = None
     if obj:
         obj_path = str(tmp_path / "scene.obj")
@@ -79,11 +100,12 @@ def test_cpp_app_matches_python_mirror(tmp_path, mode, obj):
     seg, tt, fr, img = run_demo(tmp_path, w, h, spp, bounces, frames, mode, obj_path)
 
     cam = E.Camera(position=(0.0, 0.3, 1.5), direction=(0.0, -0.1, -1.0))
-    app = E.RayTracingApp(cam, demo_settings(spp, bounces, obj_path), device=0)
+    app = E.RayTracingApp(cam, demo_settings(spp, bounces, obj_path), device=0,
+                          mode=_lib.MODE_RGBA32F if mode == "resume32" else _lib.MODE_RGBA8)
     app.open((w, h))
     if mode == "batch":
         E.compute_n_then_render(app, frames)
-    else:
+    else:  # (resume: the uninterrupted run it must equal)
         for _ in range(frames):
             E.compute_then_render(app, 1.0 / 60.0)
     st = app.context.stats()
@@ -94,3 +116,7 @@ def test_cpp_app_matches_python_mirror(tmp_path, mode, obj):
     assert (seg, tt) == (st.segments, st.tri_tests)
     assert np.array_equal(img, ref), f"{int((img != ref).any(-1).sum())} pixels differ"
     assert img[..., :3].any()  # the scene is lit
+    if mode != "resume32":  # the rgba8 accumulator against the CPU oracle on the same records
+        acc, oseg, otests = oracle_accumulator(w, h, spp, bounces, frames, obj_path, cam)
+        assert (seg, tt) == (oseg, otests)
+        assert np.array_equal(img, acc), f"{int((img != acc).any(-1).sum())} pixels differ from the oracle"

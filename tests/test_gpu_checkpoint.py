@@ -60,3 +60,26 @@ def test_load_accumulator_validation(tmp_path):
     with pytest.raises(ValueError):  # checkpoint of another image size
         other.resume(path)
     other.close()
+
+
+def test_checkpoint_on_a_context_with_a_communicator(tmp_path):
+    """RayTracingApp.checkpoint reads the local rows (HRT_IMG_LOCAL), never the collective
+    gather, so a rank joined to a communicator saves its own partition's accumulator -- the same bytes
+    as without the communicator -- and resumes from it."""
+    size = (160, 96)
+    ref, _ = render("island", size, _lib.MODE_RGBA8, None, 2, 3, tmp_path, resume=False)
+    app = E.make_app("island", num_samples=2, max_bounces=4, device=0)
+    app.open(size)
+    app.context.comm_init(E.HrtContext.comm_unique_id(), 0, 1)
+    E.compute_n_then_render(app, 2)
+    path = str(tmp_path / "comm_ckpt.npz")
+    app.checkpoint(path)
+    app.close()
+    app = E.make_app("island", num_samples=2, max_bounces=4, device=0)
+    app.open(size)
+    app.resume(path)
+    for _ in range(3):
+        E.compute_then_render(app)
+    got = app.context.read(_lib.IMG_ACCUM)
+    app.close()
+    assert np.array_equal(got, ref)
