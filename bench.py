@@ -48,8 +48,8 @@ BYTES_PER_PIXEL_FRAME = 32  # 16 B ray centre + 4 B trace store + 12 B combiner 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)   # the driver's shape: --steps 20 --warmup 5
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scene", default="island")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -276,7 +276,9 @@ def main():
         algorithmic_tf = FLOP_PER_TEST * tests_per_frame / (kern_ms * 1e-3) / 1e12
         pix_local = ctx.local_rows * W
         algo_bytes = BYTES_PER_PIXEL_FRAME * pix_local + (len(raytrace.tris) * 64 + len(raytrace.meshes) * 80)
-        roof = pmc_roofline(args, world, kernel_sym, kern_ms, tests_per_frame, ctx.local_rows / H, fpl)
+        # the timed launch's frames (the PMC record must be of the same launch shape)
+        roof = pmc_roofline(args, world, kernel_sym, kern_ms, tests_per_frame, ctx.local_rows / H,
+                            min(args.steps, fpl) if fpl > 1 else 1)
         line = {
             "metric": (f"Mrays/s ({args.scene}.obj {W}x{H} {args.spp}spp {args.bounces}-bounce path-trace segments "
                        "per second)"),
@@ -345,7 +347,7 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_roofline(args, world, kernel_sym, kern_ms, tests_per_frame, row_frac, fpl):
+def pmc_roofline(args, world, kernel_sym, kern_ms, tests_per_frame, row_frac, launch_frames):
     """roofline.achieved / frac / traffic from the committed rocprofv3 PMC record of THIS build
     (profiles/pmc_traffic.json, tools/pmc.sh): executed FP32 FLOP per frame / the live per-frame
     kernel time.  A record of another build (hrt_build_id), kernel or workload gives null."""
@@ -359,7 +361,8 @@ def pmc_roofline(args, world, kernel_sym, kern_ms, tests_per_frame, row_frac, fp
         pmc = json.load(f)
     wl = pmc.get("workload", {})
     want = {"scene": args.scene, "width": args.width, "height": args.height, "spp": args.spp,
-            "bounces": args.bounces, "kernel_variant": _lib.KERNEL_NAMES[args.variant], "frames_per_launch": fpl}
+            "bounces": args.bounces, "kernel_variant": _lib.KERNEL_NAMES[args.variant],
+            "frames_per_launch": launch_frames}
     if pmc.get("build_id") != _lib.build_id():
         out["achieved_basis"] = (f"unmeasured: the PMC record is of build {pmc.get('build_id')}, this library is "
                                  f"{_lib.build_id()}")

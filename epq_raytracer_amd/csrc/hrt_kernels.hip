@@ -30,16 +30,6 @@
 
 namespace hrt {
 
-#ifdef HRT_EXP_TWICE
-// Timing experiments only (frames unchanged): run one phase a second time on opaque copies of its
-// inputs and discard the result, so the time difference is that phase's marginal cost.
-__device__ __forceinline__ float exp_zero() {
-  float z;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-  return z;
-}
-__device__ __forceinline__ void exp_use(float v) { asm volatile("; use %0" ::"v"(v)); }
-#endif
 
 // Read-only views of the uploaded std430 records.
 struct Scene {
@@ -791,37 +781,8 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
       }
     }
   }
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 6
-  {
-    const float z = exp_zero();
-    const f3 d2 = mk(d.x + z, d.y + z, d.z + z);
-    const uint32_t o2 = (fbits(d2.x) >> 31) | ((fbits(d2.y) >> 31) << 1) | ((fbits(d2.z) >> 31) << 2);
-    exp_use((float)(uint32_t)(tl.aabb >> o2) + (float)(uint32_t)__shfl((int)tl.tsum, (int)o2, 64));
-  }
-#endif
   float best_k = c.t * kOnePlus;
   const kfloat* ct = to_const(P.cam_tris);
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 7
-  {
-    const float z = exp_zero();
-    const f3 d2 = mk(d.x + z, d.y + z, d.z + z);
-    Closest c2 = c;
-    float bk2 = best_k;
-    for (uint32_t i = 0; i < tl.n; ++i) {
-      const uint32_t e = tl.lds ? __builtin_amdgcn_readfirstlane(tl.lds[i])
-                                : (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
-      const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
-      const bool pass = prim && ((pm >> (8 * m)) & 1ull);
-      if (!__any(pass)) continue;
-      const kf16 R = ld_rec(ct, kk);
-      const float dn = pass ? dot(d2, mk(R[12], R[13], R[14])) : 0.0f;
-      if (__any(dn < 0.0f))
-        primary_exact_rec(make_float4(R[0], R[1], R[2], R[3]), make_float4(R[4], R[5], R[6], R[7]),
-                          make_float4(R[8], R[9], R[10], R[11]), dn, d2, m, c2, bk2);
-    }
-    exp_use(c2.t + (float)c2.idx);
-  }
-#endif
   for (uint32_t i = 0; i < tl.n; ++i) {
     const uint32_t e = tl.lds ? __builtin_amdgcn_readfirstlane(tl.lds[i])
                               : (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
@@ -1483,21 +1444,6 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   float best_k = c.t * kOnePlus;
   for (uint32_t k = 0; k < P.bvh_n_irregular; ++k)
     if (sec) bvh_prim_test(P.bvh_irregular, k, mask, o, d, c, bkey, best_k);
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 9
-  {
-    const float z = exp_zero();
-    const f3 d2 = mk(d.x + z, d.y + z, d.z + z);
-    unsigned long long m2 = 0ull;
-    uint32_t t2 = 0;
-    if (sec)
-      for (int m = 0; m < pc.num_meshes; ++m)
-        if (aabb_pass(sc.meshes[m], o, d2)) {
-          m2 |= 1ull << m;
-          t2 += sc.meshes[m].len;
-        }
-    exp_use((float)m2 + (float)t2);
-  }
-#endif
   float R;
   {  // farthest root-box corner from the origin, rounded up
     const float4 R0 = wq.nodes[0], R1 = wq.nodes[1];
@@ -1781,13 +1727,6 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   }
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
   const TileList tl = build_tile_list(P, active, centre, list_lds);
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 4
-  {
-    const float z = exp_zero();
-    const TileList t2 = build_tile_list(P, active, mk(centre.x + z, centre.y, centre.z), nullptr);
-    exp_use((float)t2.n + (float)t2.v + (float)t2.aabb);
-  }
-#endif
   // bounce batch threshold scaled to the item's active lanes (a split tile's row group has 8/k rows):
   // a batch of few lanes then runs alongside the other lanes' primary segments instead of after them
   const uint32_t sec_thresh = max(1u, (P.sec_batch * (uint32_t)__popcll(__ballot(active)) + 63u) / 64u);
@@ -1803,18 +1742,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
       } else {
         ++sample;
         const f3 dir = get_ray_dir(pc, centre, state);
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 2
-        {
-          uint32_t s2 = state + (uint32_t)exp_zero();
-          const f3 d2 = normalize(get_ray_dir(pc, centre, s2));
-          exp_use(d2.x + d2.y + d2.z);
-        }
-#endif
-#ifdef HRT_EXP_ONE_NORMALIZE  // timing-only experiment (wrong frames): skip the caller's second normalize
-        p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, dir, 0, true};
-#else
         p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, normalize(dir), 0, true};
-#endif
       }
     }
     const bool prim = !done && p.bounce == 0;
@@ -1835,15 +1763,6 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (any_prim) {
       if (tl.ok) {
         world_hit_tile(sc, P, tl, prim, p.pos, p.dir, tests, c);
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 1
-        {
-          const float z = exp_zero();
-          Closest c2{kFltMax, 0, 0u, 0u};
-          uint32_t t2 = 0;
-          world_hit_tile(sc, P, tl, prim, p.pos, mk(p.dir.x + z, p.dir.y + z, p.dir.z + z), t2, c2);
-          exp_use(c2.t + (float)t2 + (float)c2.idx);
-        }
-#endif
         if (D && P.diag) {
           dg.prim_considered += tl.n;
           dg.prim_survivors += tl.n;
@@ -1855,19 +1774,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (D && P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
       if constexpr (is_wq(Bounce)) {
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 5
-        const Closest c_in = c;
-#endif
         world_hit_bounce_wq<D, Bounce == kBounceWqR>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 5
-        {
-          const float z = exp_zero();
-          Closest c2 = c_in;
-          uint32_t t2 = 0;
-          world_hit_bounce_wq<D, Bounce == kBounceWqR>(sc, P, bsrc, sec, p.pos, mk(p.dir.x + z, p.dir.y + z, p.dir.z + z), t2, c2, dg);
-          exp_use(c2.t + (float)t2 + (float)c2.idx);
-        }
-#endif
       } else if constexpr (Bounce == kBounceBvh) {
         world_hit_bounce_bvh<D>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
       } else if constexpr (Bounce == kBounceCull) {
@@ -1879,15 +1786,6 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (D && P.diag) t2 = __builtin_readcyclecounter();
     if (prim || sec) {
       ++segs;
-#if defined(HRT_EXP_TWICE) && HRT_EXP_TWICE == 3
-      {
-        Path p2 = p;
-        p2.dir.x = p2.dir.x + exp_zero();
-        uint32_t s2 = state + (uint32_t)exp_zero();
-        exp_use((shade_step(sc, pc, p2, c, s2) ? 1.0f : 0.0f) + p2.dir.x + p2.dir.y + p2.dir.z + p2.light.x +
-                p2.colour.y);
-      }
-#endif
       const bool ended = shade_step(sc, pc, p, c, state);
       ++p.bounce;
       if (ended || p.bounce > pc.max_bounces) {

@@ -80,9 +80,6 @@ __device__ __forceinline__ float div_core(float num, float den, float y) {
 }
 // a / s for s > 0, correctly rounded (the shared-reciprocal path when every lane value is in range)
 __device__ __forceinline__ f3 div3(f3 a, float s) {
-#ifdef HRT_IEEE_DIV  // A/B: the compiler's sequences only
-  return {a.x / s, a.y / s, a.z / s};
-#endif
   const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
   const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
   const float sum = (a.x + a.y) + a.z;  // fmin / fmax skip a NaN component: this does not
@@ -94,9 +91,6 @@ __device__ __forceinline__ f3 div3(f3 a, float s) {
 }
 // S4: normalize = v / sqrt(dot(v, v)), correctly rounded sqrt and divides.
 __device__ __forceinline__ f3 normalize(f3 a) {
-#ifdef HRT_IEEE_DIV
-  return a / __builtin_sqrtf(dot(a, a));
-#endif
   const float d2 = dot(a, a);
   const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
   if (d2 >= 0x1p-80f && d2 <= 0x1p78f && m >= 0x1p-80f) {  // then |a.c| <= sqrt(d2) <= 2^39

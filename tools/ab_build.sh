@@ -1,12 +1,23 @@
 #!/bin/bash
 # A/B builds of libhip_raytrace.so with extra compile definitions (device and host code), for HRT_LIB=... experiments:
 #   bash tools/ab_build.sh <name> -DHRT_WQ_DEEP=0u ...   -> epq_raytracer_amd/build/ab_<name>/libhip_raytrace.so
+# EXP_PATCH=1: build from a copy of the sources with tools/exp/phase_experiments.patch applied -- the
+# timing-only phase experiments (-DHRT_EXP_TWICE=<phase>: a phase run twice on opaque copies of its inputs;
+# -DHRT_EXP_ONE_NORMALIZE: wrong frames; -DHRT_IEEE_DIV: the compiler's division sequences), which the
+# product sources do not carry.  The patch is against the sources of its commit.
 set -e
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/epq_raytracer_amd/build/ab_$NAME
 mkdir -p $OUT/obj
-make -s -C $ROOT/epq_raytracer_amd/csrc OUT=$OUT OBJDIR=$OUT/obj \
-  HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall -Wno-bitwise-instead-of-logical -mllvm -amdgpu-schedule-relaxed-occupancy=1 -I$ROOT/include -I$ROOT/epq_raytracer_amd/csrc $*" \
-  CXXFLAGS="-O2 -std=c++17 -fPIC -pthread -ffp-contract=off -fno-fast-math -Wall -Wextra -I$ROOT/include -I$ROOT/epq_raytracer_amd/csrc $*"
+SRC=$ROOT/epq_raytracer_amd/csrc
+if [ -n "$EXP_PATCH" ]; then
+  TMP=$OUT/src; rm -rf $TMP; mkdir -p $TMP/epq_raytracer_amd
+  cp -r $SRC $TMP/epq_raytracer_amd/csrc
+  (cd $TMP && patch -s -p1 < $ROOT/tools/exp/phase_experiments.patch)
+  SRC=$TMP/epq_raytracer_amd/csrc
+fi
+make -s -C $SRC OUT=$OUT OBJDIR=$OUT/obj ROOT=$ROOT \
+  HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall -Wno-bitwise-instead-of-logical -mllvm -amdgpu-schedule-relaxed-occupancy=1 -I$ROOT/include -I$SRC $*" \
+  CXXFLAGS="-O2 -std=c++17 -fPIC -pthread -ffp-contract=off -fno-fast-math -Wall -Wextra -I$ROOT/include -I$SRC $*"
 echo $OUT/libhip_raytrace.so

@@ -7,7 +7,7 @@ set -o pipefail
 TAG=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 OUT=gpurun_out/$TAG; mkdir -p $OUT
-ARGS="--warmup 2 --steps 64 --cpu-seconds 0 $*"
+ARGS="--warmup 5 --steps 20 --cpu-seconds 0 --realtime-frames 0 $*"  # the driver's bench shape
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
@@ -22,8 +22,10 @@ import json, sys
 for line in open(sys.argv[1]):
     if line.startswith("{"):
         c = json.loads(line)["config"]
+        steps = json.loads(line)["steps"]
+        c["frames_per_launch"] = min(c["frames_per_launch"], steps)  # the timed launch's frames
         print(" ".join(f"{k}={c[k]}" for k in ("scene", "width", "height", "spp", "bounces", "kernel_variant",
-                                                 "frames_per_launch")), json.loads(line)["steps"])
+                                                 "frames_per_launch")), c["frames_per_launch"])
 PY
 )
 FRAMES=${WL##* }; WL=${WL% *}
