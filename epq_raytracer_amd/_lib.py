@@ -78,7 +78,7 @@ FMT_RGBA8, FMT_RGBA32F = 0, 1
 OPT_KERNEL_VARIANT, OPT_COUNTERS, OPT_SECONDARY_BATCH, OPT_BVH_LEAF_SIZE = 1, 2, 3, 4
 OPT_SPLIT, OPT_SPLIT_FACTOR, OPT_PRIORITY, OPT_GRID_CUS, OPT_COOP, OPT_WQ_NODE_CAP, OPT_PROBE = 5, 6, 7, 8, 9, 10, 11
 OPT_FRAMES_PER_LAUNCH, OPT_OVERLAP, OPT_BUSY_SPLIT, OPT_BVH_WIDTH, OPT_WQ_NODE_RADIUS = 12, 13, 14, 15, 16
-OPT_COMM_TIMEOUT_MS = 17
+OPT_COMM_TIMEOUT_MS, OPT_DEFER_COMBINE = 17, 18
 DEBUG_OPT_FAIL_ALLOC = 1001  # libhip_raytrace_debug.so only
 DEBUG_OPT_WQ_TRI_CAP = 1002  # libhip_raytrace_debug.so only
 COMM_ID_BYTES = 128

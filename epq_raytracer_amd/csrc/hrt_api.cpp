@@ -162,10 +162,42 @@ void dev_free(hrt_context* ctx, void* p) {
   (void)hipFree(p);
 }
 
-const void* local_image(hrt_context* ctx, uint32_t image_id) {
-  if (image_id == HRT_IMG_ACCUM) return ctx->accum8 ? (const void*)ctx->accum8 : (const void*)ctx->accum32;
-  if (wait_lane(ctx, ctx->cur_lane) != HRT_OK) return nullptr;
+// The trace image: the most recent trace's ring slot, or its lane's own image.
+void* trace_image(hrt_context* ctx) {
+  if (ctx->cur_slot >= 0) return static_cast<char*>(ctx->ring) + (size_t)ctx->cur_slot * ctx->npix() * ctx->px_bytes();
   return ctx->lane[ctx->cur_lane].image();
+}
+
+const void* local_image(hrt_context* ctx, uint32_t image_id) {
+  if (image_id == HRT_IMG_ACCUM) {
+    if (flush_combines(ctx) != HRT_OK) return nullptr;
+    return ctx->accum8 ? (const void*)ctx->accum8 : (const void*)ctx->accum32;
+  }
+  if (wait_lane(ctx, ctx->cur_lane) != HRT_OK) return nullptr;
+  return trace_image(ctx);
+}
+
+hrt_status flush_combines(hrt_context* ctx) {
+  if (ctx->pend.empty()) return HRT_OK;
+  // the folds read slots that traces on every lane wrote: after each lane's latest trace
+  hrt_status st = join_lanes(ctx);
+  if (st != HRT_OK) return st;
+  const size_t np = ctx->npix(), fb = np * ctx->px_bytes();
+  for (size_t i = 0; i < ctx->pend.size();) {
+    size_t j = i;  // a run of consecutive slots (no wrap) and frames: one pass over the stack
+    while (j + 1 < ctx->pend.size() && ctx->pend[j + 1].slot == ctx->pend[j].slot + 1 &&
+           ctx->pend[j + 1].frame == ctx->pend[j].frame + 1)
+      ++j;
+    char* base = static_cast<char*>(ctx->ring) + (size_t)ctx->pend[i].slot * fb;
+    HRT_HIP(ctx, launch_accumulate_frames(ctx->accum8, ctx->accum8 ? reinterpret_cast<const uint32_t*>(base) : nullptr,
+                                          ctx->accum32, ctx->accum32 ? reinterpret_cast<const float4*>(base) : nullptr,
+                                          np, (uint32_t)(j - i + 1), ctx->pend[i].frame, ctx->stream));
+    i = j + 1;
+  }
+  ctx->pend.clear();
+  HRT_HIP(ctx, hipEventRecord(ctx->fold_done, ctx->stream));
+  ctx->fold_set = true;
+  return HRT_OK;
 }
 
 void free_scene(hrt_context* ctx, SceneBufs& s, bool keep_rays) {
@@ -309,6 +341,8 @@ extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_
     e = hrt::dev_alloc(ctx, (void**)&ctx->accum32, np * 16);
   if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(accum)"));
   if ((e = hrt::dev_alloc(ctx, (void**)&ctx->scratch, np * 16)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(scratch)"));
+  if ((e = hipEventCreateWithFlags(&ctx->fold_done, hipEventDisableTiming)) != hipSuccess)
+    return bail(hip_fail(ctx, e, "hipEventCreate(fold)"));
   if ((e = hrt::dev_alloc(ctx, (void**)&ctx->counters, hrt::kNumCounters * sizeof(unsigned long long))) != hipSuccess)
     return bail(hip_fail(ctx, e, "hipMalloc(counters)"));
   {
@@ -354,6 +388,8 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
   free_dev(ctx, ctx->counters);
   free_dev(ctx, ctx->tile_cycles);
   free_dev(ctx, ctx->frame_stack);
+  free_dev(ctx, ctx->ring);
+  if (ctx->fold_done) (void)hipEventDestroy(ctx->fold_done);
   for (int i = 0; i < 2; ++i) {
     if (ctx->staging.buf[i]) (void)hipHostFree(ctx->staging.buf[i]);
     if (ctx->staging.ev[i]) (void)hipEventDestroy(ctx->staging.ev[i]);
@@ -687,6 +723,23 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stre
   return HRT_OK;
 }
 
+// The deferred combiner's ring of frame images: up to 16 frames within 512 MiB; none (immediate
+// combines) when fewer than 4 frames fit.  Allocated once, by the first trace that needs it.
+constexpr size_t kRingBytes = (size_t)512 << 20;
+hrt_status ensure_ring(hrt_context* ctx) {
+  if (ctx->ring || ctx->ring_n == 0xFFFFFFFFu) return HRT_OK;
+  const size_t fb = ctx->npix() * ctx->px_bytes();
+  const size_t n = std::min<size_t>(16, kRingBytes / std::max<size_t>(fb, 1));
+  if (n < 4) {
+    ctx->ring_n = 0xFFFFFFFFu;  // (never: frames this large combine immediately)
+    return HRT_OK;
+  }
+  HRT_HIP(ctx, hrt::dev_alloc(ctx, &ctx->ring, n * fb));
+  ctx->ring_n = (uint32_t)n;
+  ctx->ring_next = 0;
+  return HRT_OK;
+}
+
 // The lane the next trace runs on (rotating over HRT_OPT_OVERLAP lanes, after the lane's last reader).
 hrt_status begin_lane(hrt_context* ctx, int* out) {
   const int n = ctx->diag_on ? 1 : (int)std::max(1u, ctx->overlap);
@@ -712,6 +765,17 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
   if (!pc->init && (st = check_dispatch(ctx, pc, "hrt_trace")) != HRT_OK) return st;
+  // The frame's image: the next ring slot when combines are deferred (the ring is allocated by the
+  // first such trace; a slot still waiting for its fold forces the fold first), else the lane's own.
+  int slot = -1;
+  if (!pc->init && ctx->defer) {
+    if ((st = ensure_ring(ctx)) != HRT_OK) return st;
+    if (ctx->ring) {
+      slot = (int)ctx->ring_next;
+      for (const auto& pd : ctx->pend)
+        if (pd.slot == (uint32_t)slot && (st = hrt::flush_combines(ctx)) != HRT_OK) return st;
+    }
+  }
   int l = 0;
   if ((st = begin_lane(ctx, &l)) != HRT_OK) return st;
   hrt::Lane& lane = ctx->lane[l];
@@ -719,6 +783,12 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
     HRT_HIP(ctx, hrt::launch_clear(lane.trace8, lane.trace32, ctx->npix(), lane.stream));
   } else {
     hrt::TraceParams p = make_params(ctx, pc, l);
+    if (slot >= 0) {  // after the fold that last read the slot
+      if (ctx->fold_set) HRT_HIP(ctx, hipStreamWaitEvent(lane.stream, ctx->fold_done, 0));
+      char* img = static_cast<char*>(ctx->ring) + (size_t)slot * ctx->npix() * ctx->px_bytes();
+      p.img8 = lane.trace8 ? reinterpret_cast<uint32_t*>(img) : nullptr;
+      p.img32 = lane.trace32 ? reinterpret_cast<float4*>(img) : nullptr;
+    }
     // Throughput mode: when another lane's trace is still running, this one shares the chip with it
     // (a persistent grid over 1 / HRT_OPT_BUSY_SPLIT of the CUs), so two frames' long sample chains run
     // side by side instead of the next frame waiting for every CU; an idle GPU gets the whole grid.
@@ -730,6 +800,8 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
     }
     if ((st = launch_frames(ctx, p, lane.stream, l)) != HRT_OK) return st;
   }
+  ctx->cur_slot = slot;
+  if (slot >= 0) ctx->ring_next = (uint32_t)(slot + 1) % ctx->ring_n;
   return end_lane(ctx, l);
 }
 
@@ -740,7 +812,9 @@ extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* 
   if (st != HRT_OK) return st;
   if ((st = check_dispatch(ctx, pc, "hrt_compute_n")) != HRT_OK) return st;
   if (n == 0) return HRT_OK;
-  // The whole loop runs on the context stream with lane 0's buffers, after every lane's last trace.
+  // The whole loop runs on the context stream with lane 0's buffers, after every lane's last trace
+  // and every deferred combine (frames fold in call order).
+  if ((st = hrt::flush_combines(ctx)) != HRT_OK) return st;
   if ((st = hrt::join_lanes(ctx)) != HRT_OK) return st;
   hrt::TraceParams p = make_params(ctx, pc, 0);
   hrt::Lane& lane = ctx->lane[0];
@@ -783,6 +857,7 @@ extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* 
     done += nf;
   }
   ctx->cur_lane = 0;
+  ctx->cur_slot = -1;  // the trace image is lane 0's
   ctx->lane_used = true;
   return hrt::release_lane(ctx, 0);  // lane 0's next trace follows this loop
 }
@@ -792,9 +867,22 @@ extern "C" hrt_status hrt_accumulate(hrt_context* ctx, uint32_t frame) {
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
   const int l = ctx->cur_lane;  // next_image = the most recent trace
+  if (ctx->cur_slot >= 0 && ctx->defer) {
+    // deferred: the next frame of a run of consecutive slots and frames, else the run is folded first
+    const uint32_t s = (uint32_t)ctx->cur_slot;
+    if (!ctx->pend.empty()) {
+      const hrt_context::Pend& b = ctx->pend.back();
+      if (!(s == b.slot + 1 && frame == b.frame + 1) && (st = hrt::flush_combines(ctx)) != HRT_OK) return st;
+    }
+    ctx->pend.push_back({s, frame});
+    ctx->accumulates++;
+    return HRT_OK;
+  }
+  if ((st = hrt::flush_combines(ctx)) != HRT_OK) return st;  // frames fold in call order
   if ((st = hrt::wait_lane(ctx, l)) != HRT_OK) return st;
-  const hrt::Lane& lane = ctx->lane[l];
-  HRT_HIP(ctx, hrt::launch_accumulate(ctx->accum8, lane.trace8, ctx->accum32, lane.trace32, ctx->npix(), frame,
+  void* img = hrt::trace_image(ctx);
+  HRT_HIP(ctx, hrt::launch_accumulate(ctx->accum8, ctx->accum8 ? static_cast<uint32_t*>(img) : nullptr, ctx->accum32,
+                                      ctx->accum32 ? static_cast<float4*>(img) : nullptr, ctx->npix(), frame,
                                       ctx->stream));
   ctx->accumulates++;
   return hrt::release_lane(ctx, l);
@@ -858,6 +946,7 @@ extern "C" hrt_status hrt_load_accumulator(hrt_context* ctx, uint32_t fmt, const
   if (bytes != need) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_load_accumulator: size differs from the local image");
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
+  if ((st = hrt::flush_combines(ctx)) != HRT_OK) return st;  // (overwritten below, but in call order)
   if ((st = sync_all(ctx)) != HRT_OK) return st;  // no accumulate in flight
   void* dst = ctx->accum8 ? (void*)ctx->accum8 : (void*)ctx->accum32;
   // on the context stream (non-blocking w.r.t. the null stream): the next hrt_accumulate follows it
@@ -888,6 +977,7 @@ extern "C" hrt_status hrt_synchronize(hrt_context* ctx) {
   if (!ctx) return HRT_ERR_INVALID_ARGUMENT;
   hrt_status st = bind(ctx);
   if (st != HRT_OK) return st;
+  if ((st = hrt::flush_combines(ctx)) != HRT_OK) return st;  // every accumulate has run after a sync
   return sync_all(ctx);
 }
 
@@ -1166,6 +1256,14 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       if (value < 0 || value > 2) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "wq node radius must be 0 (auto), 1 or 2");
       ctx->wq_node_radius = (uint32_t)value;
       return HRT_OK;
+    case HRT_OPT_DEFER_COMBINE: {
+      if (value < 0 || value > 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "defer combine must be 0 or 1");
+      hrt_status st = bind(ctx);
+      if (st == HRT_OK) st = hrt::flush_combines(ctx);
+      if (st != HRT_OK) return st;
+      ctx->defer = (uint32_t)value;
+      return HRT_OK;
+    }
     case HRT_OPT_COMM_TIMEOUT_MS:
       if (value < 0 || value > 0xFFFFFFFFll)
         return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "comm timeout must be in [0, 2^32) ms (0 = wait forever)");
@@ -1201,7 +1299,11 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
   }
 }
 
-extern "C" void* hrt_stream(hrt_context* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+// Work the caller enqueues on the stream follows every accumulate so far: the deferred ones are folded.
+extern "C" void* hrt_stream(hrt_context* ctx) {
+  if (!ctx || bind(ctx) != HRT_OK || hrt::flush_combines(ctx) != HRT_OK) return ctx ? (void*)ctx->stream : nullptr;
+  return (void*)ctx->stream;
+}
 
 extern "C" const char* hrt_last_error(const hrt_context* ctx) {
   return ctx ? ctx->err.c_str() : g_create_error.c_str();

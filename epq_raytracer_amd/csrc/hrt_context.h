@@ -153,6 +153,22 @@ struct hrt_context {
   };
   std::vector<Guard> guards;  // debug build: guarded device allocations (hrt_debug_check_guards)
   hrt::Staging staging;
+  // Deferred combiner (HRT_OPT_DEFER_COMBINE).  The accumulator is observable only through
+  // hrt_read_image / hrt_stream / hrt_synchronize, so hrt_accumulate after an hrt_trace only records
+  // (ring slot, frame): the trace wrote a slot of a ring of frame images instead of its lane's image,
+  // and the recorded frames are folded in frame order (accumulate_frames_*, the hrt_compute_n combiner)
+  // at the next observation or when the ring is full -- the per-frame combine's bytes, without a
+  // combiner kernel queued between every two traces.
+  void* ring = nullptr;        // ring_n frame images (context format), allocated by the first trace
+  uint32_t ring_n = 0, ring_next = 0;
+  int cur_slot = -1;           // ring slot of the most recent trace (-1: its lane's own image)
+  struct Pend {
+    uint32_t slot, frame;
+  };
+  std::vector<Pend> pend;      // recorded, not yet folded (consecutive slots and frames)
+  hipEvent_t fold_done = nullptr;  // recorded on `stream` after the last fold (a slot's next trace waits)
+  bool fold_set = false;
+  uint32_t defer = 1;          // HRT_OPT_DEFER_COMBINE
   hrt::Comm* comm = nullptr;  // hrt_comm_init / hrt_comm_init_all
   uint32_t comm_timeout_ms = 120000;  // HRT_OPT_COMM_TIMEOUT_MS (0: wait forever)
 
@@ -173,8 +189,11 @@ void dev_free(hrt_context* ctx, void* p);
 hrt_status join_lanes(hrt_context* ctx);         // the context stream waits for every lane's trace
 hrt_status wait_lane(hrt_context* ctx, int l);   // ... for lane l's trace
 hrt_status release_lane(hrt_context* ctx, int l);  // lane l's buffers are free after the stream's work so far
-// Reads image_id of this context's local rows in its own pixel format, ordered on ctx->stream.
+// Reads image_id of this context's local rows in its own pixel format, ordered on ctx->stream (the
+// accumulator after every deferred combine has been folded).
 const void* local_image(hrt_context* ctx, uint32_t image_id);
+// Folds the deferred combines (hrt_context::pend) into the accumulator on ctx->stream.
+hrt_status flush_combines(hrt_context* ctx);
 // dst <- npix pixels at src (context format) converted to fmt via scratch, ordered on ctx->stream; blocking.
 hrt_status copy_frame_out(hrt_context* ctx, const void* src, size_t npix, uint32_t fmt, void* dst, void* scratch);
 // hrt_read_image on a context with a communicator (hrt_comm.cpp); arg = the caller's own argument

@@ -80,3 +80,23 @@ def mismatch_report(a: np.ndarray, b: np.ndarray) -> str:
         return "identical"
     y, x = diff[0]
     return f"{len(diff)} pixels differ; first at (x={x}, y={y}): {a[y, x]} vs {b[y, x]}"
+
+
+GOLDEN_FULL = os.path.join(ROOT, "tests", "golden", "golden_full.json")
+
+
+def golden_full(name: str) -> dict:
+    """Whole-frame oracle digests at the BASELINE sizes (tests/golden/make_golden_full.py)."""
+    import json
+    with open(GOLDEN_FULL) as f:
+        return json.load(f)["frames"][name]
+
+
+def assert_frame_digest(img: np.ndarray, rec: dict, what: str) -> None:
+    """img's SHA-256 equals the oracle's whole-frame digest; on a mismatch, name the rows that differ."""
+    import hashlib
+    if hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest() == rec["sha256_rgba8"]:
+        return
+    bad = [y for y in range(img.shape[0])
+           if hashlib.sha256(np.ascontiguousarray(img[y]).tobytes()).hexdigest()[:16] != rec["row_sha256_16"][y]]
+    raise AssertionError(f"{what}: the frame differs from the oracle's in {len(bad)} rows (first {bad[:10]})")

@@ -58,3 +58,25 @@ def test_fma_and_generic_oracle_builds_agree():
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, check=True)
         outs.append(r.stdout.strip())
     assert outs[0] == outs[1] and len(outs[0]) == 64
+
+
+def test_whole_frame_digests_reproduced_on_sampled_rows():
+    """tests/golden/golden_full.json (the oracle's whole-frame digests at the BASELINE sizes, which the
+    GPU suite hashes its 1080p frames against) is reproduced by the oracle on sampled rows: the row
+    digests of the headline and C3 frames, and the C4 accumulator rows through the combiner."""
+    full = json.load(open(os.path.join(GOLD, "golden_full.json")))["frames"]
+    for name, scene in (("headline", "island"), ("c3", "cave")):
+        m = full[name]
+        case = SceneCase(scene, tuple(m["size"]), m["spp"], m["bounces"], rng_offset=m["rng_offset"])
+        for y in (0, 541):
+            img = case.oracle(rows=(y, y + 1))[0]
+            assert hashlib.sha256(img[y].tobytes()).hexdigest()[:16] == m["row_sha256_16"][y], (name, y)
+    m = full["c4"]
+    y = 620
+    acc = np.zeros((1, m["size"][0], 4), np.uint8)
+    pyoracle.accumulate_rgba8(0, acc, acc.copy())
+    for k in m["frames"]:
+        img = SceneCase("island", tuple(m["size"]), m["spp"], m["bounces"]).oracle(rng_offset=k, rows=(y, y + 1))[0]
+        pyoracle.accumulate_rgba8(k, acc, np.ascontiguousarray(img[y:y + 1]))
+    assert hashlib.sha256(acc[0].tobytes()).hexdigest()[:16] == m["row_sha256_16"][y]
+    assert len(m["row_sha256_16"]) == m["size"][1] == 1080

@@ -66,6 +66,54 @@ def test_overlapped_realtime_loop_is_byte_exact(scene, size, spp, variant, mode)
             (batched[2].segments, batched[2].tri_tests, batched[2].traces, batched[2].accumulates)
 
 
+@pytest.mark.parametrize("mode", [_lib.MODE_RGBA8, _lib.MODE_RGBA32F])
+def test_deferred_combines_equal_immediate_ones(mode):
+    """HRT_OPT_DEFER_COMBINE: the realtime loop's combines recorded and folded
+    in frame order later equal one combiner dispatch per hrt_accumulate, byte for byte -- across a
+    ring wrap (40 frames > 16 slots), reads of both images in between (the accumulator read folds),
+    a trace read before its accumulate, an accumulate of the same image twice, a trace that is never
+    accumulated, hrt_compute_n and a checkpoint restore in the middle, and the counters."""
+    case = SceneCase("island", (96, 64), 2, 8)
+    fmt = _lib.FMT_RGBA8 if mode == _lib.MODE_RGBA8 else _lib.FMT_RGBA32F
+
+    def run(defer):
+        ctx = case.context(mode=mode)
+        ctx.set_option(_lib.OPT_DEFER_COMBINE, defer)
+        seen = []
+        for k in range(1, 41):
+            ctx.trace(case.push(k))
+            if k % 7 == 0:
+                seen.append(ctx.read(_lib.IMG_TRACE, fmt))
+            ctx.accumulate(k)
+            if k % 11 == 0:
+                seen.append(ctx.read(_lib.IMG_ACCUM, fmt))
+            if k == 13:
+                ctx.accumulate(k + 100)  # the same trace image again
+            if k == 17:
+                ctx.trace(case.push(999))  # never accumulated: the next accumulate takes the next trace
+        ctx.compute_n(case.push(41), 3)
+        saved = ctx.read(_lib.IMG_ACCUM, fmt)
+        for k in range(44, 50):
+            ctx.trace(case.push(k))
+            ctx.accumulate(k)
+        ctx.load_accumulator(saved)
+        for k in range(44, 47):
+            ctx.trace(case.push(k))
+            ctx.accumulate(k)
+        st = ctx.stats()
+        out = ctx.read(_lib.IMG_ACCUM, fmt), ctx.read(_lib.IMG_TRACE, fmt), seen
+        ctx.close()
+        return out, (st.segments, st.tri_tests, st.traces, st.accumulates)
+
+    (acc0, tr0, seen0), st0 = run(0)
+    (acc1, tr1, seen1), st1 = run(1)
+    assert st0 == st1
+    assert np.array_equal(acc0.view(np.uint8), acc1.view(np.uint8))
+    assert np.array_equal(tr0.view(np.uint8), tr1.view(np.uint8))
+    assert len(seen0) == len(seen1) and all(np.array_equal(a.view(np.uint8), b.view(np.uint8))
+                                            for a, b in zip(seen0, seen1))
+
+
 def test_overlapped_traces_read_back_in_order():
     """Every trace image read between overlapped traces is that frame's oracle frame."""
     case = SceneCase("island", (80, 48), 2, 8)

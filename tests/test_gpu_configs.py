@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import pyoracle
-from helpers import E, SceneCase, _lib, mismatch_report
+from helpers import E, SceneCase, _lib, assert_frame_digest, golden_full, mismatch_report
 from epq_raytracer_amd import rowtiles
 
 pytestmark = pytest.mark.gpu
@@ -50,6 +50,14 @@ def test_c3_cave_rows_match_oracle(cave_frame):
         assert np.array_equal(img[y], ref[y]), f"row {y}: " + mismatch_report(img[y:y + 1], ref[y:y + 1])
 
 
+def test_c3_cave_whole_frame_matches_oracle(cave_frame):
+    """The whole C3 frame against the oracle's digest and exact counters (make_golden_full.py)."""
+    _, (img, st), _ = cave_frame
+    rec = golden_full("c3")
+    assert (st.segments, st.tri_tests) == (rec["segments"], rec["tri_tests"])
+    assert_frame_digest(img, rec, "C3 cave")
+
+
 def test_c3_cave_full_frame_matches_literal_kernel(cave_frame):
     _, (img, st), (lit, lst) = cave_frame
     assert np.array_equal(img, lit), mismatch_report(img, lit)
@@ -87,6 +95,10 @@ def test_c4_island_eight_row_tile_parts_gathered():
     assert (segs, tests) == (wst.segments, wst.tri_tests)
     assert np.array_equal(local[rowtiles.assembly_index(1080, 8, 8)], want)
     assert np.array_equal(got, want), mismatch_report(got, want)
+    # the whole gathered 4-frame accumulator against the oracle's (clear, trace k + combine(k), k = 1..4)
+    rec = golden_full("c4")
+    assert (segs, tests) == (rec["segments"], rec["tri_tests"])
+    assert_frame_digest(got, rec, "C4 accumulator")
     rng = np.random.default_rng(4)
     ys = np.repeat([5, 400, 560, 700, 1070], 48)
     xs = rng.integers(0, 1920, len(ys))

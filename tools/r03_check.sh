@@ -15,3 +15,9 @@ timeout -k 10 120 python3 bench.py --gpus 2 --steps 4 > $OUT/bench_n2_nccl.json 
 echo "rccl --gpus 2 on one GPU: exit $? ($(tail -1 $OUT/bench_n2_nccl.err))"
 timeout -k 10 600 python3 bench.py --cpu-seconds 5 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
+# optional A/B of library builds (AB_LIBS="libA libB ..."): interleaved per-frame times, island and cave
+if [ -n "$AB_LIBS" ]; then
+  timeout -k 10 600 bash tools/ab.sh ${AB_ROUNDS:-2} $AB_LIBS -- --scene cave > $OUT/ab_cave.jsonl 2>&1 || { echo "ab cave failed"; tail -5 $OUT/ab_cave.jsonl; exit 1; }
+  timeout -k 10 600 bash tools/ab.sh ${AB_ROUNDS:-2} $AB_LIBS > $OUT/ab_island.jsonl 2>&1 || { echo "ab island failed"; tail -5 $OUT/ab_island.jsonl; exit 1; }
+  python3 tools/ab_summary.py $OUT/ab_cave.jsonl $OUT/ab_island.jsonl
+fi

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--lanes", type=int, nargs="+", default=[1, 2, 3])
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--busy-split", type=int, nargs="+", default=[2], help="HRT_OPT_BUSY_SPLIT values")
+    ap.add_argument("--defer", type=int, nargs="+", default=[1], help="HRT_OPT_DEFER_COMBINE values")
     ap.add_argument("--grid-cus", type=int, nargs="+", default=[0],
                     help="HRT_OPT_GRID_CUS values (libhip_raytrace_debug.so; 0 = every CU)")
     a = ap.parse_args()
@@ -34,7 +35,9 @@ def main():
     ctx = case.context(debug=debug)
     k = 1
     for r in range(a.rounds):
-        for lanes, cus, bs in [(n, c, b) for n in a.lanes for c in a.grid_cus for b in a.busy_split]:
+        for lanes, cus, bs, df in [(n, c, b, d) for n in a.lanes for c in a.grid_cus for b in a.busy_split
+                                   for d in a.defer]:
+            ctx.set_option(_lib.OPT_DEFER_COMBINE, df)
             ctx.set_option(_lib.OPT_OVERLAP, lanes)
             ctx.set_option(_lib.OPT_BUSY_SPLIT, bs)
             if debug:
@@ -51,7 +54,8 @@ def main():
                 k += 1
             ctx.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / a.frames
-            print(json.dumps({"round": r, "lanes": lanes, "grid_cus": cus, "busy_split": bs, "ms_per_frame": round(ms, 3)}), flush=True)
+            print(json.dumps({"round": r, "lanes": lanes, "grid_cus": cus, "busy_split": bs, "defer": df,
+                              "ms_per_frame": round(ms, 3)}), flush=True)
         if debug:
             ctx.set_option(_lib.OPT_GRID_CUS, 0)
         ctx.synchronize()
