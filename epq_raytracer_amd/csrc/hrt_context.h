@@ -168,7 +168,7 @@ struct hrt_context {
   std::vector<Pend> pend;      // recorded, not yet folded (consecutive slots and frames)
   hipEvent_t fold_done = nullptr;  // recorded on `stream` after the last fold (a slot's next trace waits)
   bool fold_set = false;
-  uint32_t defer = 1;          // HRT_OPT_DEFER_COMBINE
+  uint32_t defer = 0;          // HRT_OPT_DEFER_COMBINE (off: measured slower, hip_raytrace.h)
   hrt::Comm* comm = nullptr;  // hrt_comm_init / hrt_comm_init_all
   uint32_t comm_timeout_ms = 120000;  // HRT_OPT_COMM_TIMEOUT_MS (0: wait forever)
 

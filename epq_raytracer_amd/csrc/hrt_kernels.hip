@@ -31,6 +31,13 @@
 namespace hrt {
 
 
+#ifndef HRT_SHADE_KARGS
+#define HRT_SHADE_KARGS 1  // shading reads the scene pointers from the kernel arguments (kargs)
+#endif
+#ifndef HRT_RAYGEN_KARGS
+#define HRT_RAYGEN_KARGS 1  // the camera read per sample from the kernel arguments (kargs)
+#endif
+
 // Read-only views of the uploaded std430 records.
 struct Scene {
   const float4* __restrict__ rays;
@@ -40,18 +47,38 @@ struct Scene {
   const float4* __restrict__ nhat;  // normalize(tri.normal) per triangle (tri_normals, same arithmetic)
 };
 
+// The kernel arguments through an opaque pointer to the kernarg segment: a field read through it is
+// a scalar load at the point of use that the compiler cannot hoist out of the fused loop.  Constants
+// needed only inside a phase (a bounce batch, a work item) are read this way at the phase's start, so
+// they occupy SGPRs for the phase only instead of for the whole kernel (where ~120 of them were
+// spilled into VGPR lanes and read back with v_readlane).
+typedef const __attribute__((address_space(4))) TraceParams* KArgs;
+__device__ __forceinline__ KArgs kargs() {
+  KArgs p = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+// The scene's pointers read at the point of use (shading: after a segment, not held across the loop).
+__device__ __forceinline__ Scene kscene() {
+  const KArgs K = kargs();
+  return Scene{K->rays, K->spheres, K->tris, K->meshes, K->tri_nhat};
+}
+
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 __device__ __forceinline__ f3 ray_at(f3 o, f3 d, float t) { return o + d * t; }  // :158-160
 
 // local (compacted) row -> global row, hrt_create_info partition.
-__device__ __forceinline__ uint32_t global_row(uint32_t lr, const TraceParams& p) {
-  if (p.part_count <= 1) return lr;
-  const uint32_t tile = lr / p.row_tile, r = lr - tile * p.row_tile;
-  return (tile * p.part_count + p.part_index) * p.row_tile + r;
+__device__ __forceinline__ uint32_t global_row(uint32_t lr, const TraceParams& /*P*/) {
+  const KArgs K = kargs();  // (once per work item)
+  const uint32_t parts = K->part_count, rt = K->row_tile;
+  if (parts <= 1) return lr;
+  const uint32_t tile = lr / rt, r = lr - tile * rt;
+  return (tile * parts + K->part_index) * rt + r;
 }
 
 // get_ray_dir, raytracing.glsl:162-166 (u1, u2, u3 in that order)
-__device__ __forceinline__ f3 get_ray_dir(const hrt_push_constants& pc, f3 c, uint32_t& state) {
+template <class PC>
+__device__ __forceinline__ f3 get_ray_dir(const PC& pc, f3 c, uint32_t& state) {
   const float r = (u01(hash(state)) * 2.0f) * 3.14159265358979323846f;
   float sr, cr;
   spec_sincos_angle(r, sr, cr);  // r in [0, 2pi]
@@ -61,7 +88,7 @@ __device__ __forceinline__ f3 get_ray_dir(const hrt_push_constants& pc, f3 c, ui
   const float s3 = sqrt_rng(u01(hash(state)));
   const f3 t2 = ((mk(0.0f, 1.0f, 0.0f) * sr) * j) * s3;
   const f3 nc = (c + t1) + t2;
-  const float* M = pc.cam_alignment_mat;
+  const auto& M = pc.cam_alignment_mat;
   const f3 w = mk(__builtin_fmaf(M[8], nc.z, __builtin_fmaf(M[4], nc.y, M[0] * nc.x)),
                   __builtin_fmaf(M[9], nc.z, __builtin_fmaf(M[5], nc.y, M[1] * nc.x)),
                   __builtin_fmaf(M[10], nc.z, __builtin_fmaf(M[6], nc.y, M[2] * nc.x)));
@@ -251,13 +278,14 @@ __device__ __forceinline__ bool shade_step(const Scene& sc, const hrt_push_const
   return true;
 }
 
-__device__ __forceinline__ void store_pixel(const TraceParams& P, uint32_t x, uint32_t lr, f3 col,
+__device__ __forceinline__ void store_pixel(const TraceParams& /*P*/, uint32_t x, uint32_t lr, f3 col,
                                             uint32_t frame = 0) {
-  const size_t idx = (size_t)lr * P.pc.width + x + frame * P.frame_stride;
-  if (P.img8) {
-    P.img8[idx] = unorm8(col.x) | (unorm8(col.y) << 8) | (unorm8(col.z) << 16) | (255u << 24);
-  }
-  if (P.img32) P.img32[idx] = make_float4(col.x, col.y, col.z, 1.0f);
+  const KArgs K = kargs();  // (once per work item)
+  const size_t idx = (size_t)lr * K->pc.width + x + frame * K->frame_stride;
+  uint32_t* img8 = K->img8;
+  float4* img32 = K->img32;
+  if (img8) img8[idx] = unorm8(col.x) | (unorm8(col.y) << 8) | (unorm8(col.z) << 16) | (255u << 24);
+  if (img32) img32[idx] = make_float4(col.x, col.y, col.z, 1.0f);
 }
 
 // wave-level sums of the per-lane counters (+ the wave's longest lane), in every lane.
@@ -273,17 +301,18 @@ __device__ __forceinline__ void wave_counters(uint32_t segs, uint32_t tests, uns
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
   }
 }
-__device__ __forceinline__ void add_counters(const TraceParams& P, unsigned long long s, unsigned long long t,
+__device__ __forceinline__ void add_counters(const TraceParams& /*P*/, unsigned long long s, unsigned long long t,
                                              unsigned long long mx) {
-  if (P.counters && (threadIdx.x & 63) == 0) {
-    atomicAdd(&P.counters[0], s);
-    atomicAdd(&P.counters[1], t);
-    atomicAdd(&P.counters[2], mx);
+  unsigned long long* counters = kargs()->counters;
+  if (counters && (threadIdx.x & 63) == 0) {
+    atomicAdd(&counters[0], s);
+    atomicAdd(&counters[1], t);
+    atomicAdd(&counters[2], mx);
   }
 }
 // one atomic each per wave
 __device__ __forceinline__ void flush_counters(const TraceParams& P, uint32_t segs, uint32_t tests) {
-  if (!P.counters) return;
+  if (!kargs()->counters) return;
   unsigned long long s, t;
   uint32_t mx;
   wave_counters(segs, tests, s, t, mx);
@@ -666,7 +695,7 @@ __device__ __forceinline__ void aabb_truth_table(const TraceParams& P, TileList&
   bool pass = false, bad = false;
   uint32_t len = 0;
   if (m < (uint32_t)pc.num_meshes) {
-    const hrt_mesh& mesh = P.meshes[m];
+    const hrt_mesh& mesh = kargs()->meshes[m];
     for (int a = 0; a < 3; ++a) {
       const float ov = a == 0 ? o.x : (a == 1 ? o.y : o.z);
       const float lo = mesh.min_point[a] - ov, hi = mesh.max_point[a] - ov;
@@ -729,11 +758,15 @@ __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool a
   if (!ok) return t;
   aabb_truth_table(P, t);
   const uint32_t lane = threadIdx.x & 63;
+  const KArgs K = kargs();  // (once per work item)
+  const uint32_t* cam_start = K->cam_start;
+  const uint32_t* cam_count = K->cam_count;
+  const float4* cam_cull = K->cam_cull;
   for (int m = 0; m < pc.num_meshes; ++m) {
-    const uint32_t k0 = P.cam_start[m], k1 = k0 + P.cam_count[m];
+    const uint32_t k0 = cam_start[m], k1 = k0 + cam_count[m];
     for (uint32_t base = k0; base < k1; base += 64) {
       const uint32_t k = base + lane;
-      const bool keep = k < k1 && bundle_keep(P.cam_cull, k, b);
+      const bool keep = k < k1 && bundle_keep(cam_cull, k, b);
       unsigned long long mask = __ballot(keep);
       const uint32_t cnt = (uint32_t)__popcll(mask);
       if (t.n + cnt > cap) return t;  // ok stays false: per-iteration cull
@@ -1246,6 +1279,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // hold key 0 and win ties, as they are scanned first).  A child is dropped only by BUNDLE_BVH's exact
 // node test (wq_node_visit) against the slot's current t, which only ever exceeds the final one.
 // When the node stack could overflow, the popped groups' subtrees are walked stacklessly instead.
+#ifndef HRT_WQ_CONE_NR
+#define HRT_WQ_CONE_NR 1  // ... in trace_bundle_wq_nr (per-node radius: the enclosed scenes)
+#endif
 #ifndef HRT_WQ_CONE
 #define HRT_WQ_CONE 1    // the nodes' back-face (normal cone) test
 #endif
@@ -1254,6 +1290,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #endif
 #ifndef HRT_WQ_BAND_CHUNK
 #define HRT_WQ_BAND_CHUNK 1  // band rounds whose loads are issued together (2 / 4 / 8 measured slower: r02t)
+#endif
+#ifndef HRT_WQ_LEAN_SHFL
+#define HRT_WQ_LEAN_SHFL 1  // node-only steps skip the mesh-filter shuffles; abs_t = abs_coef * R recomputed
 #endif
 #ifndef HRT_WQ_TRI_MIN
 #define HRT_WQ_TRI_MIN 64u  // a triangle step runs once this many triangle pairs wait (or no node pair is left)
@@ -1355,7 +1394,8 @@ __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& 
   const float x = __builtin_fmaf(half_lo(w9), q.d.z, __builtin_fmaf(half_hi(w8), q.d.y, half_lo(w8) * q.d.x));
   const float xa = fmaxf(fabsf(x) - (2e-6f + kWqAxisErr), 0.0f);
   const float s_up = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-xa, xa, 1.0f), 0.0f)) + 1.2e-6f;
-  if (HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back
+  if ((NodeR ? HRT_WQ_CONE_NR : HRT_WQ_CONE) && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f)
+    return false;  // back
   float Rm = q.R;
   if constexpr (NodeR) {  // trace_bundle_wq_nr (HRT_OPT_WQ_NODE_RADIUS)
     // R for this member: the ray origin's distance to the farthest corner of its box (every vertex
@@ -1404,9 +1444,8 @@ __device__ __forceinline__ float wq_slot_t(const WqLds& wq, uint32_t r) {
 }
 
 // Leaf prim k for ray r (origin o, direction d, mesh filter mask): test and lower the ray's slot.
-__device__ __forceinline__ void wq_leaf_prim(const TraceParams& P, const WqLds& wq, uint32_t k, uint32_t r,
+__device__ __forceinline__ void wq_leaf_prim(const float4* __restrict__ pr, const WqLds& wq, uint32_t k, uint32_t r,
                                              unsigned long long mask, f3 o, f3 d) {
-  const float4* pr = P.bvh_prims;
   const float4 A = pr[4 * k], B = pr[4 * k + 1], C = pr[4 * k + 2], N = pr[4 * k + 3];
   const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
   float dist;
@@ -1427,6 +1466,11 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
                                                     f3 o, f3 d, uint32_t& tests, Closest& c, Diag& dg) {
   const hrt_push_constants& pc = P.pc;
   const uint32_t lane = threadIdx.x & 63;
+  // the batch's constants, read here (kargs): live for the batch only
+  const KArgs K = kargs();
+  const float4* prims = K->bvh_prims;
+  const float rel_t = K->bvh_rel_t, abs_coef = K->bvh_abs_coef;
+  const uint32_t tcap = K->wq_tcap;
   spheres_first(sc, pc, sec, o, d, c);
   const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // the meshes' AABB tests and the traversal
   unsigned long long mask = 0ull;
@@ -1442,8 +1486,10 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   // the irregular list: per lane, as in BUNDLE_BVH
   uint32_t bkey = 0;
   float best_k = c.t * kOnePlus;
-  for (uint32_t k = 0; k < P.bvh_n_irregular; ++k)
-    if (sec) bvh_prim_test(P.bvh_irregular, k, mask, o, d, c, bkey, best_k);
+  const uint32_t n_irr = K->bvh_n_irregular;
+  const float4* irr = K->bvh_irregular;
+  for (uint32_t k = 0; k < n_irr; ++k)
+    if (sec) bvh_prim_test(irr, k, mask, o, d, c, bkey, best_k);
   float R;
   {  // farthest root-box corner from the origin, rounded up
     const float4 R0 = wq.nodes[0], R1 = wq.nodes[1];
@@ -1451,7 +1497,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const float fz = fmaxf(fabsf(o.z - R0.z), fabsf(R1.z - o.z));
     R = __builtin_amdgcn_sqrtf(fx * fx + fy * fy + fz * fz) * 1.0001f;  // 1 ulp, inside the x1.0001
   }
-  const float abs_t = P.bvh_abs_coef * R;
+  const float abs_t = abs_coef * R;
   uint32_t band_tests = 0, band_lmax = 0;
   // the ray's closest hit so far (spheres, the irregular list) seeds its slot
   const uint32_t id0 = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
@@ -1464,7 +1510,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const unsigned long long rm =
         ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
         (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
-    wq_leaf_prim(P, wq, e >> 6, r, rm, shfl3(o, r), shfl3(d, r));
+    wq_leaf_prim(prims, wq, e >> 6, r, rm, shfl3(o, r), shfl3(d, r));
     tri_pairs += 64u;
     ++steps;
   };
@@ -1478,9 +1524,10 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     uint32_t b0 = 0, n = 0;
     const BandCheck bc(d, -kBandTau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
     if (sec && mask) {
-      const uint32_t cell = dir_cell(d, P.bvh_dir_res);
-      b0 = P.bvh_band_off[cell];
-      n = P.bvh_band_off[cell + 1] - b0;
+      const uint32_t* band_off = K->bvh_band_off;
+      const uint32_t cell = dir_cell(d, K->bvh_dir_res);
+      b0 = band_off[cell];
+      n = band_off[cell + 1] - b0;
     }
     if (D && P.diag) {
       dg.band_len += n;
@@ -1497,6 +1544,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     // rounds in chunks of kBandChunk: every round's owner search and entry load issued before any
     // round's check, so the chunk waits for its (mostly L2-missing) entry loads once
     constexpr int kBandChunk = HRT_WQ_BAND_CHUNK;
+    const uint2* band = K->bvh_band;
     for (uint32_t base = 0; base < total; base += 64u * kBandChunk) {
       uint32_t own[kBandChunk];
       uint2 q[kBandChunk];
@@ -1514,12 +1562,12 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         }
         own[rr] = lo;
         const uint32_t k = (uint32_t)__shfl((int)b0, (int)lo, 64) + (gi - pl);
-        q[rr] = gi < total ? P.bvh_band[k] : make_uint2(0u, 0u);
+        q[rr] = gi < total ? band[k] : make_uint2(0u, 0u);
       }
 #pragma unroll
       for (int rr = 0; rr < kBandChunk; ++rr) {
         if (base + 64u * rr >= total) break;  // wave-uniform
-        if (tc + 64u > P.wq_tcap) tri_step64();  // room for this round's pairs
+        if (tc + 64u > tcap) tri_step64();  // room for this round's pairs
         BandCheck oc = bc;
         oc.ds = shfl3(bc.ds, own[rr]);
         const bool push = base + 64u * rr + lane < total && oc.in(q[rr]);
@@ -1536,7 +1584,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   if (sec && mask) {
     float tn;
     rinfo = wq_info(wq.nodes, 0);
-    rvis = wq_node_visit(wq.nodes, o, d, inv, R, abs_t, c.t * (1.0f + P.bvh_rel_t) + abs_t, tn);
+    rvis = wq_node_visit(wq.nodes, o, d, inv, R, abs_t, c.t * (1.0f + rel_t) + abs_t, tn);
   }
   const uint32_t rcnt = rvis ? rinfo >> 27 : 0u;
   const unsigned long long rb = __ballot(rvis && rcnt == 0u);
@@ -1553,7 +1601,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     for (uint32_t j = 0; j < rcnt; ++j) wq.ts[pre + j] = (((rinfo & 0x07FFFFFFu) + j) << 6) | lane;
     tc += tot;
   }
-  const uint32_t width = P.bvh_wq_width;  // the image's largest group
+  const uint32_t width = K->bvh_wq_width;  // the image's largest group
   uint32_t node_pairs = 0;
   while (nc | tc) {
     ++steps;
@@ -1573,17 +1621,23 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const uint32_t e = is_node ? wq.ns[nc + lane] : is_tri ? wq.ts[tc + lane - nn] : lane;
     const uint32_t r = e & 63u;
     const f3 ro = shfl3(o, r), rd = shfl3(d, r);
-    const unsigned long long rm =
-        ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
-        (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
-    if (is_tri) wq_leaf_prim(P, wq, e >> 6, r, rm, ro, rd);
+    // the ray's mesh filter: for triangle pairs, and for the node pairs' in-place fallbacks (a step that
+    // could overflow the node stack: known here; a leaf burst beyond the triangle stack: fetched there)
+    const bool overflow = nc + width * nn > wq.ncap;  // wave-uniform
+    const bool rm_now = !HRT_WQ_LEAN_SHFL || tn > 0u || (nn > 0u && overflow);  // wave-uniform
+    auto ray_mask = [&]() {  // (all 64 lanes active)
+      return ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
+             (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
+    };
+    unsigned long long rm = rm_now ? ray_mask() : 0ull;
+    if (is_tri) wq_leaf_prim(prims, wq, e >> 6, r, rm, ro, rd);
     if (nn == 0u) continue;
     // node pairs (ray r, group fc .. fc + cnt - 1): test every member.  Slot k: member k's push entry
     // (its info word << 6 | r when a kept inner node, else ~0u), sort key (minus its box entry
     // distance when pushed, else -inf), and its triangle count when a kept leaf.
     const f3 rinv = shfl3(inv, r);
-    const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
-    const bool overflow = nc + width * nn > wq.ncap;  // wave-uniform
+    const float rR = __shfl(R, (int)r, 64);
+    const float rabs = HRT_WQ_LEAN_SHFL ? abs_coef * rR : __shfl(abs_t, (int)r, 64);  // = the owner's abs_t
     const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs);
     uint32_t pe[kWqSlots], li[kWqSlots];
     float pk[kWqSlots];
@@ -1596,7 +1650,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     if (is_node) {
       const uint32_t g = e >> 6, fc = g & 0xFFFFu, gcnt = (g >> 16) + 1u;
       if (!overflow) {
-        const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
+        const float t_hi = wq_slot_t(wq, r) * (1.0f + rel_t) + rabs;
         auto member = [&](const float4& N0, const float4& N1, const float4& N2, int k) {
           float tnear;
           const uint32_t inf = __builtin_bit_cast(uint32_t, N2.w);
@@ -1632,11 +1686,11 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         while (cur != end) {
           const uint32_t inf = wq_info(wq.nodes, cur), cnt = inf >> 27;
           float tnear;
-          const float t_hi = wq_slot_t(wq, r) * (1.0f + P.bvh_rel_t) + rabs;
+          const float t_hi = wq_slot_t(wq, r) * (1.0f + rel_t) + rabs;
           const bool v = wq_node_visit(wq.nodes + 3 * cur, ro, rd, rinv, rR, rabs, t_hi, tnear);
           if (v && cnt) {
             const uint32_t first = inf & 0x07FFFFFFu;
-            for (uint32_t k = first; k < first + cnt; ++k) wq_leaf_prim(P, wq, k, r, rm, ro, rd);
+            for (uint32_t k = first; k < first + cnt; ++k) wq_leaf_prim(prims, wq, k, r, rm, ro, rd);
           }
           cur = (v && !cnt) ? (inf & 0xFFFFu) : wq_escape(wq.nodes, cur);  // inner: its first child
         }
@@ -1662,7 +1716,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       pre += lanes_below(bb) << b;
       tot += (uint32_t)__popcll(bb) << b;
     }
-    if (tc + tot <= P.wq_tcap) {  // wave-uniform
+    if (tc + tot <= tcap) {  // wave-uniform
       uint32_t at = tc + pre;
 #pragma unroll
       for (int k = 0; k < (int)kWqSlots; ++k) {
@@ -1672,10 +1726,11 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       }
       tc += tot;
     } else {  // a burst of kept leaves beyond the triangle stack: each lane tests its own in place
+      if (!rm_now) rm = ray_mask();
 #pragma unroll
       for (int k = 0; k < (int)kWqSlots; ++k) {
         const uint32_t c = li[k] >> 27, first = li[k] & 0x07FFFFFFu;
-        for (uint32_t j = 0; j < c; ++j) wq_leaf_prim(P, wq, first + j, r, rm, ro, rd);
+        for (uint32_t j = 0; j < c; ++j) wq_leaf_prim(prims, wq, first + j, r, rm, ro, rd);
       }
     }
   }
@@ -1715,21 +1770,23 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
   const uint32_t y = global_row(lr, P);
   uint32_t segs = 0, tests = 0;
-  const bool active = x < pc.width && lr < P.local_rows && y < pc.height;
+  const bool active = x < pc.width && lr < kargs()->local_rows && y < pc.height;
   const uint32_t id = active ? x + y * pc.width : 0u;
   const uint64_t tile_t0 = (D && P.tile_cycles) ? __builtin_readcyclecounter() : 0;
   f3 colour = mk(0.0f, 0.0f, 0.0f);
   uint32_t state = (pc.rng_offset + frame) * 719393u + id;  // raytracing.glsl:376, frame f of the launch
   f3 centre = mk(0.0f, 0.0f, 0.0f);
   if (active) {
-    const float4 rc = sc.rays[id];
+    const float4 rc = kargs()->rays[id];
     centre = mk(rc.x, rc.y, rc.z);
   }
+#if !HRT_RAYGEN_KARGS
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
+#endif
   const TileList tl = build_tile_list(P, active, centre, list_lds);
   // bounce batch threshold scaled to the item's active lanes (a split tile's row group has 8/k rows):
   // a batch of few lanes then runs alongside the other lanes' primary segments instead of after them
-  const uint32_t sec_thresh = max(1u, (P.sec_batch * (uint32_t)__popcll(__ballot(active)) + 63u) / 64u);
+  const uint32_t sec_thresh = max(1u, (kargs()->sec_batch * (uint32_t)__popcll(__ballot(active)) + 63u) / 64u);
   int sample = 0;
   Path p;
   p.bounce = pc.max_bounces + 1;
@@ -1741,8 +1798,17 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
         done = true;
       } else {
         ++sample;
+#if HRT_RAYGEN_KARGS
+        // the camera (matrix, jitter, position) read at the sample's start (kargs): 13 values not held
+        // in SGPRs across the loop
+        const KArgs K = kargs();
+        const f3 dir = get_ray_dir(K->pc, centre, state);
+        p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), mk(K->pc.cam_pos[0], K->pc.cam_pos[1], K->pc.cam_pos[2]),
+                 normalize(dir), 0, true};
+#else
         const f3 dir = get_ray_dir(pc, centre, state);
         p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, normalize(dir), 0, true};
+#endif
       }
     }
     const bool prim = !done && p.bounce == 0;
@@ -1762,7 +1828,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (co.w == 0) co.work += 2u + (any_prim ? 1u + (tl.ok ? tl.n : 64u) : 0u);  // shading, primary list
     if (any_prim) {
       if (tl.ok) {
-        world_hit_tile(sc, P, tl, prim, p.pos, p.dir, tests, c);
+        world_hit_tile(HRT_SHADE_KARGS ? kscene() : sc, P, tl, prim, p.pos, p.dir, tests, c);
         if (D && P.diag) {
           dg.prim_considered += tl.n;
           dg.prim_survivors += tl.n;
@@ -1774,7 +1840,8 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (D && P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
       if constexpr (is_wq(Bounce)) {
-        world_hit_bounce_wq<D, Bounce == kBounceWqR>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
+        world_hit_bounce_wq<D, Bounce == kBounceWqR>(HRT_SHADE_KARGS ? kscene() : sc, P, bsrc, sec, p.pos, p.dir, tests,
+                                                     c, dg);
       } else if constexpr (Bounce == kBounceBvh) {
         world_hit_bounce_bvh<D>(sc, P, bsrc, sec, p.pos, p.dir, tests, c, dg);
       } else if constexpr (Bounce == kBounceCull) {
@@ -1786,7 +1853,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (D && P.diag) t2 = __builtin_readcyclecounter();
     if (prim || sec) {
       ++segs;
-      const bool ended = shade_step(sc, pc, p, c, state);
+      const bool ended = shade_step(HRT_SHADE_KARGS ? kscene() : sc, pc, p, c, state);
       ++p.bounce;
       if (ended || p.bounce > pc.max_bounces) {
         colour = colour + p.light * p.colour;
@@ -1986,12 +2053,13 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     const bool refill = cur >= end;  // wave-uniform
     const uint32_t g = (uint64_t)cur + 16ull * kGrab * resident < n ? kGrab : 1u;
     uint32_t t = 0;
+    const KArgs K = kargs();  // (per work item: not held across the item's fused loop)
     if (lane == 0) {
       // a tile's cost: its items' summed clocks; the heavy threshold's sum counts an item by its
       // share of the tile's lanes (its work), so splitting does not raise the threshold (with summed
       // clocks there too, borderline tiles flipped between split and whole: 7.4 / 8.4 ms frames)
-      if (prev_tile != 0xFFFFFFFFu) atomicAdd(&P.tile_cost[prev_tile], prev_cost);
-      if (refill) t = first + atomicAdd(&P.sched[0], g);
+      if (prev_tile != 0xFFFFFFFFu) atomicAdd(&K->tile_cost[prev_tile], prev_cost);
+      if (refill) t = first + atomicAdd(&K->sched[0], g);
     }
     if (prev_tile != 0xFFFFFFFFu) cost_sum += prev_cost >> prev_lk;
     if (refill) {
@@ -2001,8 +2069,9 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     t = cur++;
     if (t >= n) break;
     const uint32_t ti = t / nf, tf = t - ti * nf;
-    const uint32_t item = P.items ? __builtin_amdgcn_readfirstlane(P.items[ti]) : 0u;
-    const uint32_t tile = P.items ? item & kItemTileMask : ti, lk = (item >> 22) & 7u, sub = (item >> 25) & 63u;
+    const uint32_t* items = K->items;
+    const uint32_t item = items ? __builtin_amdgcn_readfirstlane(items[ti]) : 0u;
+    const uint32_t tile = items ? item & kItemTileMask : ti, lk = (item >> 22) & 7u, sub = (item >> 25) & 63u;
     const bool hot = item >> 31;  // heavy last time: issue priority over the light tiles' waves
     const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
     const uint32_t j = (sub << (6u - lk)) + lane;  // the tile pixel (row-major) of this lane

@@ -256,12 +256,14 @@ typedef enum hrt_option {
    * agreement or the gather before it aborts the communicator (ncclCommAbort) and returns
    * HRT_ERR_COMM (default 120000; 0 = wait forever).  Per context. */
   HRT_OPT_COMM_TIMEOUT_MS = 17,
-  /* hrt_trace + hrt_accumulate (the realtime loop): 1 (default) = the combine of a traced frame is
-   * deferred -- the trace writes a slot of a ring of up to 16 frame images (allocated by the first
-   * trace, at most 512 MiB) and the recorded frames are folded into the accumulator in frame order at
-   * the next hrt_read_image / hrt_synchronize / hrt_stream / hrt_compute_n or when the ring is full, so
-   * no combiner kernel waits between two traces; 0 = one combiner dispatch per hrt_accumulate.  The
-   * bytes are the same either way. */
+  /* hrt_trace + hrt_accumulate (the realtime loop): 1 = the combine of a traced frame is deferred --
+   * the trace writes a slot of a ring of up to 16 frame images (allocated by the first trace, at most
+   * 512 MiB) and the recorded frames are folded into the accumulator in frame order at the next
+   * hrt_read_image / hrt_synchronize / hrt_stream / hrt_compute_n or when the ring is full, so no
+   * combiner kernel waits between two traces; 0 (default) = one combiner dispatch per hrt_accumulate.
+   * The bytes are the same either way.  Measured on island 1080p (r03b): 2.81-2.86 ms per frame
+   * deferred against 2.53 immediate -- without the combiners pacing them, the three lanes' persistent
+   * traces all run at once and contend for the CUs -- so it is off by default. */
   HRT_OPT_DEFER_COMBINE = 18,
   /* libhip_raytrace_debug.so only (tests): the value-th device allocation of the next hrt_set_scene
    * fails with HRT_ERR_OUT_OF_MEMORY (0 = off) */
