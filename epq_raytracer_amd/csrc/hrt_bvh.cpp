@@ -215,7 +215,7 @@ struct Builder {
     // box margin for a lane whose origin is within R of every scene vertex: mg = a + b R, from
     // eta = 6e + (1.01 rho + 3.2e + 18.4e G R) / (tau_g - rho - 4e-7) (DESIGN.md "BVH cull"), plus
     // 4e x the box's largest coordinate for the kernel's rounding of lo - mg / hi + mg
-    const double eps = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)kBandTau - rho - 4e-7);
+    const double eps = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)out.band_tau - rho - 4e-7);
     const double coord = std::max({std::fabs(box.lo.x), std::fabs(box.lo.y), std::fabs(box.lo.z),
                                    std::fabs(box.hi.x), std::fabs(box.hi.y), std::fabs(box.hi.z)});
     const double a_m = 2.02 * ext * (6 * eps + (1.01 * rho + 3.2 * eps) * inv_tp) + 4 * eps * coord;
@@ -286,14 +286,14 @@ Cone cell_cone(int f, double u0, double u1, double v0, double v1) {
   return {c, std::cos(r), std::sin(r)};
 }
 
-// Is d.nhat in the grazing band (-kBandTau - 1e-5, 2e-5) for some d in the cap?  With
+// Is d.nhat in the grazing band (-tau - 1e-5, 2e-5) for some d in the cap?  With
 // theta = angle(c, nhat): d.nhat ranges over [cos(min(pi, theta + r)), cos(max(0, theta - r))].
-bool cone_hits_band(const Cone& k, V3 nhat) {
+bool cone_hits_band(const Cone& k, V3 nhat, double tau) {
   const double x = std::max(-1.0, std::min(1.0, dot(k.c, nhat)));
   const double y = std::sqrt(std::max(0.0, 1.0 - x * x));
   const double hi = (x >= k.cr) ? 1.0 : x * k.cr + y * k.sr;
   const double lo = (x <= -k.cr) ? -1.0 : x * k.cr - y * k.sr;
-  return hi > -((double)kBandTau + 1e-5) && lo < 2e-5;
+  return hi > -(tau + 1e-5) && lo < 2e-5;
 }
 
 // The cell itself (a convex spherical quad): corners in order and its edges' planes.  The exact range
@@ -317,9 +317,9 @@ Quad cell_quad(int f, double u0, double u1, double v0, double v1) {
   }
   return q;
 }
-// Is d.nhat in the grazing band (-kBandTau - 1e-5, 2e-5) for some d of the quad widened by 1e-4 rad
+// Is d.nhat in the grazing band (-tau - 1e-5, 2e-5) for some d of the quad widened by 1e-4 rad
 // (the kernel's dir_cell rounding; moving d by an angle e moves d.nhat by at most e)?
-bool quad_hits_band(const Quad& q, V3 n) {
+bool quad_hits_band(const Quad& q, V3 n, double tau) {
   double hi = -2.0, lo = 2.0;
   for (int i = 0; i < 4; ++i) {
     const double v = dot(q.c[i], n);
@@ -344,7 +344,7 @@ bool quad_hits_band(const Quad& q, V3 n) {
   if (in_p) hi = 1.0;
   if (in_m) lo = -1.0;
   constexpr double kWiden = 1e-4 + 1e-9;
-  return hi + kWiden > -((double)kBandTau + 1e-5) && lo - kWiden < 2e-5;
+  return hi + kWiden > -(tau + 1e-5) && lo - kWiden < 2e-5;
 }
 
 void build_band_lists(BvhHost& out) {
@@ -370,14 +370,14 @@ void build_band_lists(BvhHost& out) {
     const Cone kc = cone_of(f, kCoarse, cu, cv);
     std::vector<uint32_t> coarse, mid;
     for (uint32_t k = 0; k < out.n_prims; ++k)
-      if (cone_hits_band(kc, nh[k])) coarse.push_back(k);
+      if (cone_hits_band(kc, nh[k], out.band_tau)) coarse.push_back(k);
     for (int mu = 0; mu < kSubMid; ++mu) {
       for (int mv = 0; mv < kSubMid; ++mv) {
         const int ju = cu * kSubMid + mu, jv = cv * kSubMid + mv;
         const Cone mc = cone_of(f, kMid, ju, jv);
         mid.clear();
         for (uint32_t k : coarse)
-          if (cone_hits_band(mc, nh[k])) mid.push_back(k);
+          if (cone_hits_band(mc, nh[k], out.band_tau)) mid.push_back(k);
         for (int su = 0; su < kSub; ++su) {
           for (int sv = 0; sv < kSub; ++sv) {
             const int iu = ju * kSub + su, iv = jv * kSub + sv;
@@ -385,7 +385,7 @@ void build_band_lists(BvhHost& out) {
                                       -1.0 + 2.0 * iv / kDirRes, -1.0 + 2.0 * (iv + 1) / kDirRes);
             std::vector<uint32_t>& l = lists[((size_t)f * kDirRes + iu) * kDirRes + iv];
             for (uint32_t k : mid)
-              if (quad_hits_band(fq, nh[k])) l.push_back(k);
+              if (quad_hits_band(fq, nh[k], out.band_tau)) l.push_back(k);
           }
         }
       }
@@ -528,8 +528,9 @@ bool make_wq_nodes(const BvhHost& b, std::vector<float>& out, uint32_t width, ui
 }
 
 bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
-               uint32_t leaf_size, BvhHost& out, uint32_t wq_width) {
+               uint32_t leaf_size, BvhHost& out, uint32_t wq_width, float band_tau) {
   out = BvhHost{};
+  out.band_tau = band_tau;
   if (n_meshes > kBvhMaxMeshes) return false;
   uint64_t total = 0;
   for (uint32_t m = 0; m < n_meshes; ++m) total += meshes[m].len;
@@ -621,7 +622,7 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
   out.dir_res = (uint32_t)dir_res_for(out.n_prims);
   build_band_lists(out);
   // t-slack of the box test for a lane at distance <= R: abs = abs_coef R, rel
-  const double e = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)kBandTau - out.rho_max - 4e-7);
+  const double e = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)out.band_tau - out.rho_max - 4e-7);
   out.abs_coef = round_up(2.1 * (4.2 * e + out.rho_max) * inv_tp * (1.0 + 1e-6));
   out.rel_t = round_up((2.1 * (3.2 * e + out.rho_max) * inv_tp + 4 * e) * (1.0 + 1e-6));
   out.wq_ok = make_wq_nodes(out, out.wq_nodes, wq_width, &out.wq_n_nodes, &out.wq_width);

@@ -70,6 +70,7 @@ struct TraceParams {
   uint32_t n_frames;
   size_t frame_stride;
   uint32_t bvh_node_r;  // BUNDLE_WQ: trace_bundle_wq_nr, box margins with a per-node R (HRT_OPT_WQ_NODE_RADIUS)
+  float bvh_band_tau;   // the grazing band's width tau_g the hierarchy and band lists were built for
 };
 
 // Per device, once: the dynamic-LDS limits of the persistent kernels (hipFuncSetAttribute).

@@ -1026,7 +1026,7 @@ __device__ __forceinline__ void world_hit_bounce_cull(const Scene& sc, const Tra
 // Each bounce lane walks the BVH (hrt_bvh.h) in preorder with escape indices (one register of
 // state).  For a triangle (a, e1, e2, n) and the lane's ray (o, d), |d| = 1 (DESIGN.md "BVH cull"):
 //   back     d.n^ >= 2e-5: the reference's dn = d.n rounds to > 0 and raytracing.glsl:219 rejects;
-//   band     -kBandTau - 1e-5 < d.n^ < 2e-5: grazing; the reference's arithmetic is rounding noise
+//   band     -tau_g - 1e-5 < d.n^ < 2e-5 (tau_g = P.bvh_band_tau, the scene's): grazing; the reference's arithmetic is rounding noise
 //            there and may accept anywhere in the triangle's plane, so these triangles are listed per
 //            cube-map direction cell (hrt_bvh.cpp build_band_lists) and every lane tests its cell's
 //            list exactly;
@@ -1211,9 +1211,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
   if (sec && mask) {
     const uint32_t cell = dir_cell(d, P.bvh_dir_res);
     const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
-    // Pre-check: an entry whose decoded d.n^ is outside (-kBandTau - 2e-5, 3e-5) widened by the
-    // quantization error is not in this lane's band (-kBandTau - 1e-5, 2e-5).
-    const BandCheck bc(d, -kBandTau - 2e-5f, 3e-5f);
+    // Pre-check: an entry whose decoded d.n^ is outside (-tau_g - 2e-5, 3e-5) widened by the
+    // quantization error is not in this lane's band (-tau_g - 1e-5, 2e-5).
+    const BandCheck bc(d, -P.bvh_band_tau - 2e-5f, 3e-5f);
     uint32_t k = b0;
     for (; k + 4 <= b1; k += 4) {
       const uint2 qs[4] = {P.bvh_band[k], P.bvh_band[k + 1], P.bvh_band[k + 2], P.bvh_band[k + 3]};
@@ -1279,9 +1279,6 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // hold key 0 and win ties, as they are scanned first).  A child is dropped only by BUNDLE_BVH's exact
 // node test (wq_node_visit) against the slot's current t, which only ever exceeds the final one.
 // When the node stack could overflow, the popped groups' subtrees are walked stacklessly instead.
-#ifndef HRT_WQ_CONE_NR
-#define HRT_WQ_CONE_NR 1  // ... in trace_bundle_wq_nr (per-node radius: the enclosed scenes)
-#endif
 #ifndef HRT_WQ_CONE
 #define HRT_WQ_CONE 1    // the nodes' back-face (normal cone) test
 #endif
@@ -1290,9 +1287,6 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #endif
 #ifndef HRT_WQ_BAND_CHUNK
 #define HRT_WQ_BAND_CHUNK 1  // band rounds whose loads are issued together (2 / 4 / 8 measured slower: r02t)
-#endif
-#ifndef HRT_WQ_LEAN_SHFL
-#define HRT_WQ_LEAN_SHFL 1  // node-only steps skip the mesh-filter shuffles; abs_t = abs_coef * R recomputed
 #endif
 #ifndef HRT_WQ_TRI_MIN
 #define HRT_WQ_TRI_MIN 64u  // a triangle step runs once this many triangle pairs wait (or no node pair is left)
@@ -1394,8 +1388,8 @@ __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& 
   const float x = __builtin_fmaf(half_lo(w9), q.d.z, __builtin_fmaf(half_hi(w8), q.d.y, half_lo(w8) * q.d.x));
   const float xa = fmaxf(fabsf(x) - (2e-6f + kWqAxisErr), 0.0f);
   const float s_up = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-xa, xa, 1.0f), 0.0f)) + 1.2e-6f;
-  if ((NodeR ? HRT_WQ_CONE_NR : HRT_WQ_CONE) && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f)
-    return false;  // back
+  // (the cone test pays on cave too with per-node radii: without it 7.25 -> 7.43 ms, r03c)
+  if (HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back
   float Rm = q.R;
   if constexpr (NodeR) {  // trace_bundle_wq_nr (HRT_OPT_WQ_NODE_RADIUS)
     // R for this member: the ray origin's distance to the farthest corner of its box (every vertex
@@ -1522,7 +1516,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   // minimum is the per-lane scan's result.
   if (__any(sec && mask)) {
     uint32_t b0 = 0, n = 0;
-    const BandCheck bc(d, -kBandTau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
+    const BandCheck bc(d, -K->bvh_band_tau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
     if (sec && mask) {
       const uint32_t* band_off = K->bvh_band_off;
       const uint32_t cell = dir_cell(d, K->bvh_dir_res);
@@ -1621,23 +1615,19 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const uint32_t e = is_node ? wq.ns[nc + lane] : is_tri ? wq.ts[tc + lane - nn] : lane;
     const uint32_t r = e & 63u;
     const f3 ro = shfl3(o, r), rd = shfl3(d, r);
-    // the ray's mesh filter: for triangle pairs, and for the node pairs' in-place fallbacks (a step that
-    // could overflow the node stack: known here; a leaf burst beyond the triangle stack: fetched there)
-    const bool overflow = nc + width * nn > wq.ncap;  // wave-uniform
-    const bool rm_now = !HRT_WQ_LEAN_SHFL || tn > 0u || (nn > 0u && overflow);  // wave-uniform
-    auto ray_mask = [&]() {  // (all 64 lanes active)
-      return ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
-             (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
-    };
-    unsigned long long rm = rm_now ? ray_mask() : 0ull;
+    const unsigned long long rm =
+        ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
+        (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
     if (is_tri) wq_leaf_prim(prims, wq, e >> 6, r, rm, ro, rd);
     if (nn == 0u) continue;
     // node pairs (ray r, group fc .. fc + cnt - 1): test every member.  Slot k: member k's push entry
     // (its info word << 6 | r when a kept inner node, else ~0u), sort key (minus its box entry
     // distance when pushed, else -inf), and its triangle count when a kept leaf.
+    // (r03, measured slower: fetching the mesh filter only for steps with triangle pairs and abs_t as
+    // abs_coef * R instead of a shuffle -- island 2.271 -> 2.276, cave 7.248 -> 7.310 ms)
     const f3 rinv = shfl3(inv, r);
-    const float rR = __shfl(R, (int)r, 64);
-    const float rabs = HRT_WQ_LEAN_SHFL ? abs_coef * rR : __shfl(abs_t, (int)r, 64);  // = the owner's abs_t
+    const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
+    const bool overflow = nc + width * nn > wq.ncap;  // wave-uniform
     const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs);
     uint32_t pe[kWqSlots], li[kWqSlots];
     float pk[kWqSlots];
@@ -1726,7 +1716,6 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       }
       tc += tot;
     } else {  // a burst of kept leaves beyond the triangle stack: each lane tests its own in place
-      if (!rm_now) rm = ray_mask();
 #pragma unroll
       for (int k = 0; k < (int)kWqSlots; ++k) {
         const uint32_t c = li[k] >> 27, first = li[k] & 0x07FFFFFFu;
