@@ -12,6 +12,9 @@
 #ifndef HRT_BVH_SWEEP
 #define HRT_BVH_SWEEP 1  // full-sweep SAH splits (0: 16 bins per axis)
 #endif
+#ifndef HRT_BVH_SAH_R
+#define HRT_BVH_SAH_R 0.0  // > 0: the SAH costs boxes grown by their triangles' margins at this x the scene diagonal
+#endif
 
 namespace hrt {
 namespace {
@@ -48,6 +51,7 @@ struct Box {
 // One regular (mesh, triangle) entry.
 struct Entry {
   Box box;
+  Box sbox;        // what the SAH sees: box grown by the triangle's own margin at R = kSahR x the scene diagonal
   V3 centroid;
   V3 nhat;         // n_rec / |n_rec|
   double g;        // max(|e1|, |e2|) / |n_rec|
@@ -92,14 +96,21 @@ struct Builder {
     out.nodes.resize((size_t)out.n_nodes * 16, 0.0f);
     Box box, cbox;
     V3 axis{0, 0, 0};
-    double g = 0, rho = 0, ext = 0;
+    // box margin for a lane whose origin is within R of every vertex below: each triangle i needs
+    // 2 eta_i ext_i = a_i + b_i R, eta_i = 6e + (1.01 rho_i + 3.2e + 18.4e G_i R) / (tau_g - rho_i - 4e-7)
+    // (DESIGN.md "BVH cull"), so the node takes max_i a_i and max_i b_i -- per triangle, not the
+    // product of the subtree's largest extent and largest G (r02 and before), which charged a big
+    // triangle with a small triangle's G (cave: 2x wider margins)
+    const double eps = 5.9604644775390625e-08;
+    double rho = 0, a_tri = 0, b_tri = 0;
     for (uint32_t i = b; i < b + n; ++i) {
       box.grow(e[i].box);
       cbox.grow(e[i].centroid);
       axis = axis + e[i].nhat;
-      g = std::max(g, e[i].g);
       rho = std::max(rho, e[i].rho);
-      ext = std::max(ext, e[i].ext);
+      const double inv_tpi = 1.02 / ((double)out.band_tau - e[i].rho - 4e-7);
+      a_tri = std::max(a_tri, 2.02 * e[i].ext * (6 * eps + (1.01 * e[i].rho + 3.2 * eps) * inv_tpi));
+      b_tri = std::max(b_tri, 2.02 * e[i].ext * 18.4 * eps * e[i].g * inv_tpi);
     }
     // normal cone around the mean direction
     double cphi = 0.0, sphi = 1.0;
@@ -136,12 +147,12 @@ struct Builder {
         });
         Box acc;
         for (uint32_t i = n; i-- > 1;) {
-          acc.grow(e[b + i].box);
+          acc.grow(e[b + i].sbox);
           right_area[i] = acc.area();
         }
         Box left;
         for (uint32_t i = 1; i < n; ++i) {
-          left.grow(e[b + i - 1].box);
+          left.grow(e[b + i - 1].sbox);
           const double cost = left.area() * i + right_area[i] * (n - i);
           if (cost < best) {
             best = cost;
@@ -212,14 +223,11 @@ struct Builder {
 #endif
     }
 
-    // box margin for a lane whose origin is within R of every scene vertex: mg = a + b R, from
-    // eta = 6e + (1.01 rho + 3.2e + 18.4e G R) / (tau_g - rho - 4e-7) (DESIGN.md "BVH cull"), plus
-    // 4e x the box's largest coordinate for the kernel's rounding of lo - mg / hi + mg
-    const double eps = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)out.band_tau - rho - 4e-7);
+    // mg = a + b R, plus 4e x the box's largest coordinate for the kernel's rounding of lo - mg / hi + mg
     const double coord = std::max({std::fabs(box.lo.x), std::fabs(box.lo.y), std::fabs(box.lo.z),
                                    std::fabs(box.hi.x), std::fabs(box.hi.y), std::fabs(box.hi.z)});
-    const double a_m = 2.02 * ext * (6 * eps + (1.01 * rho + 3.2 * eps) * inv_tp) + 4 * eps * coord;
-    const double b_m = 2.02 * ext * 18.4 * eps * g * inv_tp;
+    const double a_m = a_tri + 4 * eps * coord;
+    const double b_m = b_tri;
     out.rho_max = std::max(out.rho_max, rho);
     float* r = &out.nodes[(size_t)node * 16];
     r[0] = round_down(box.lo.x);
@@ -587,6 +595,18 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
     }
   }
   if (!entries.empty()) {
+    // the SAH's boxes: each triangle's box grown by its own margin a_i + b_i R at a typical R
+    Box scene;
+    for (const Entry& en : entries) scene.grow(en.box);
+    const double R_sah = HRT_BVH_SAH_R * norm(scene.hi - scene.lo), eps = 5.9604644775390625e-08;
+    for (Entry& en : entries) {
+      const double inv_tpi = 1.02 / ((double)out.band_tau - en.rho - 4e-7);
+      const double m = R_sah > 0.0 ? 2.02 * en.ext * (6 * eps + (1.01 * en.rho + 3.2 * eps + 18.4 * eps * en.g * R_sah) * inv_tpi)
+                                   : 0.0;
+      en.sbox = en.box;
+      en.sbox.lo = en.sbox.lo - V3{m, m, m};
+      en.sbox.hi = en.sbox.hi + V3{m, m, m};
+    }
     Builder bld{entries, leaf_size, out};
     bld.build(0, (uint32_t)entries.size(), tris);
   }
