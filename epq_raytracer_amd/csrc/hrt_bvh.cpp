@@ -13,7 +13,7 @@
 #define HRT_BVH_SWEEP 1  // full-sweep SAH splits (0: 16 bins per axis)
 #endif
 #ifndef HRT_BVH_SAH_R
-#define HRT_BVH_SAH_R 0.0  // > 0: the SAH costs boxes grown by their triangles' margins at this x the scene diagonal
+#define HRT_BVH_SAH_R 0.25  // the SAH costs boxes grown by their triangles' margins at this x the scene diagonal (0: plain boxes)
 #endif
 
 namespace hrt {

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--sec-batch", type=int, default=0)
     ap.add_argument("--leaf", type=int, default=0, help="> 0: BVH leaf size (HRT_OPT_BVH_LEAF_SIZE)")
     ap.add_argument("--width", type=int, default=0, help="> 0: BUNDLE_WQ group width (HRT_OPT_BVH_WIDTH)")
+    ap.add_argument("--node-r", type=int, default=0, help="HRT_OPT_WQ_NODE_RADIUS (0 auto, 1 scene-wide R, 2 per node)")
     ap.add_argument("--batch", type=int, default=0,
                     help="> 0: each measurement is hrt_compute_n of this many frames (ms = per frame, wall incl. accumulates)")
     a = ap.parse_args()
@@ -40,7 +41,7 @@ def main():
     ctx = case.context(variant=a.variant, partition=part,
                        options={_lib.OPT_COOP: a.coop, _lib.OPT_SPLIT_FACTOR: a.factor, _lib.OPT_PRIORITY: a.prio,
                                 _lib.OPT_SPLIT: a.split, _lib.OPT_SECONDARY_BATCH: a.sec_batch,
-                                _lib.OPT_WQ_NODE_CAP: a.ncap, _lib.OPT_PROBE: a.probe,
+                                _lib.OPT_WQ_NODE_CAP: a.ncap, _lib.OPT_PROBE: a.probe, _lib.OPT_WQ_NODE_RADIUS: a.node_r,
                                 **({_lib.OPT_BVH_LEAF_SIZE: a.leaf} if a.leaf > 0 else {}),
                                 **({_lib.OPT_BVH_WIDTH: a.width} if a.width > 0 else {})},
                        debug=a.prio == 2)  # heavy tiles only: a libhip_raytrace_debug.so diagnostics mode
@@ -64,7 +65,7 @@ def main():
         ms.append(round(ctx.stats().total_trace_ms, 3))
     ctx.close()
     print(json.dumps({"batch": a.batch, "scene": a.scene, "variant": a.variant, "partition": a.partition, "coop": a.coop, "factor": a.factor,
-                      "split": a.split, "sec_batch": a.sec_batch, "ncap": a.ncap, "probe": a.probe, "leaf": a.leaf, "width": a.width, "prio": a.prio, "ms": ms}))
+                      "split": a.split, "sec_batch": a.sec_batch, "ncap": a.ncap, "probe": a.probe, "node_r": a.node_r, "leaf": a.leaf, "width": a.width, "prio": a.prio, "ms": ms}))
 
 
 if __name__ == "__main__":
