@@ -511,17 +511,7 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
     ++leaf;
     built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, bvh, ctx->bvh_width);
   }
-  // an enclosed scene (wide margins at kBandTau) is rebuilt with the wider grazing band, which narrows
-  // its margins (hrt_bvh.h kBandTauWide); HRT_SCENE_BVH_MARGIN_MILLI keeps the kBandTau figure
   const double margin_frac = bvh.margin_frac;
-  if (built && margin_frac * 1000.0 > hrt::kNodeRadiusMarginMilli) {
-    hrt::BvhHost wide;
-    if (hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, wide, ctx->bvh_width, hrt::kBandTauWide) &&
-        (!bvh.wq_ok || (wide.wq_ok && hrt::wq_stack_cap(wide.wq_n_nodes, wide.wq_width, leaf) >=
-                                          std::min(hrt::kAutoLeafWqStack,
-                                                   hrt::wq_stack_cap(bvh.wq_n_nodes, bvh.wq_width, leaf)))))
-      bvh = std::move(wide);
-  }
   if (built) {
     auto up = [&](auto*& dst, const auto& v, const char* what) -> hrt_status {
       return alloc_upload(ctx, alloc, (void**)&dst, v.data(), v.size() * sizeof(v[0]), what);
@@ -546,6 +536,7 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   s.bvh_info[HRT_SCENE_BVH_MARGIN_MILLI] = (uint32_t)std::min(1e9, margin_frac * 1000.0 + 0.5);
   s.bvh_abs_coef = bvh.abs_coef;
   s.bvh_band_tau = built ? bvh.band_tau : hrt::kBandTau;
+  s.bvh_margin_c0 = bvh.margin_c0;
   s.bvh_rel_t = bvh.rel_t;
   s.bvh_dir_res = bvh.dir_res;
   s.bvh_built_leaf = std::max(1u, std::min(leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
@@ -668,6 +659,7 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.bvh_abs_coef = s.bvh_abs_coef;
   p.bvh_rel_t = s.bvh_rel_t;
   p.bvh_band_tau = s.bvh_band_tau;
+  p.bvh_margin_c0 = s.bvh_margin_c0;
   p.bvh_node_r = ctx->wq_node_radius == 2 ||
                  (ctx->wq_node_radius == 0 && s.bvh_info[HRT_SCENE_BVH_MARGIN_MILLI] > hrt::kNodeRadiusMarginMilli);
   p.bvh_n_irregular = s.bvh_info[HRT_SCENE_BVH_IRREGULAR];

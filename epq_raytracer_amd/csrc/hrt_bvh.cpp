@@ -638,6 +638,14 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
       msum += ((double)r[3] + (double)r[7] * R) / ext;
     }
     out.margin_frac = out.n_nodes ? msum / out.n_nodes : 0.0;
+    // the tau-free part of a node margin (2.02 x 6 eps x ext_i + 4 eps x the box's largest coordinate),
+    // bounded over the scene: the kernel's cone-scaled margin adds it unscaled
+    double ext_max = 0.0;
+    for (const Entry& en : entries) ext_max = std::max(ext_max, en.ext);
+    const double coord_max = std::max({std::fabs((double)r0[0]), std::fabs((double)r0[1]), std::fabs((double)r0[2]),
+                                       std::fabs((double)r0[4]), std::fabs((double)r0[5]), std::fabs((double)r0[6])});
+    const double eps = 5.9604644775390625e-08;
+    out.margin_c0 = round_up((2.02 * 6 * eps * ext_max + 4 * eps * coord_max) * 1.01);
   }
   out.dir_res = (uint32_t)dir_res_for(out.n_prims);
   build_band_lists(out);

@@ -51,6 +51,7 @@ struct BvhHost {
   double rho_max = 0.0;
   float abs_coef = 0.0f, rel_t = 0.0f;  // box-test t-slack: [-abs_coef R, best (1 + rel_t) + abs_coef R]
   float band_tau = 0.0f;            // the grazing band's width tau_g this hierarchy was built for
+  float margin_c0 = 0.0f;           // >= every node's tau-free margin part: 12.12 eps ext_i + 4 eps coord
 };
 
 // auto HRT_OPT_WQ_NODE_RADIUS: per-node R above this HRT_SCENE_BVH_MARGIN_MILLI (island 26 / island@4 69:
@@ -61,14 +62,10 @@ constexpr uint32_t kNodeRadiusMarginMilli = 100;
 #define HRT_BAND_TAU 4.5e-3f
 #endif
 constexpr float kBandTau = HRT_BAND_TAU;
-// tau_g trades the nodes' box margins (~ 1 / tau_g) against the band lists' length (~ cell + tau_g); the
-// enclosed scenes whose margins are wide (HRT_SCENE_BVH_MARGIN_MILLI above kNodeRadiusMarginMilli at
-// kBandTau: cave) are rebuilt with this one (r03a re-sweep with per-node radii: cave 4.5e-3 / 6e-3 /
-// 9e-3 / 1.2e-2 -> 7.28 / 7.18 / 7.69 / 7.53 ms per frame; island 4.5e-3 best, profiles/r03/).
-#ifndef HRT_BAND_TAU_WIDE
-#define HRT_BAND_TAU_WIDE 6e-3f
-#endif
-constexpr float kBandTauWide = HRT_BAND_TAU_WIDE;
+// (tau_g trades the nodes' box margins, ~ 1 / tau_g, against the band lists' length, ~ cell + tau_g.
+// r03: with per-triangle margins 4.5e-3 is best on cave as well -- 4.5e-3 / 6e-3 / 9e-3: 6.36 / 6.43 /
+// 6.62 ms per frame, profiles/r03/r03f_*; build_bvh takes it as a parameter, the kernels read it from
+// TraceParams::bvh_band_tau.)
 // Grazing-band entries (8 B): prim index (18 bits, kBvhMaxEntries) | round(n^x * kBandQx) as a signed
 // 14-bit field << 18; round(n^y * kBandQyz) | round(n^z * kBandQyz) << 16, signed 16-bit fields.
 // |n^ - decoded| <= 0.5 / kBandQx in x, 0.5 / kBandQyz in y, z: |d.n^ - d.decoded| <= 6.2e-5 for |d| = 1,

@@ -1279,6 +1279,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // hold key 0 and win ties, as they are scanned first).  A child is dropped only by BUNDLE_BVH's exact
 // node test (wq_node_visit) against the slot's current t, which only ever exceeds the final one.
 // When the node stack could overflow, the popped groups' subtrees are walked stacklessly instead.
+#ifndef HRT_WQ_CONE_MARGIN
+#define HRT_WQ_CONE_MARGIN 1  // node margins scaled by the normal cone's bound on -d.n^ (wq_member_visit)
+#endif
 #ifndef HRT_WQ_CONE
 #define HRT_WQ_CONE 1    // the nodes' back-face (normal cone) test
 #endif
@@ -1361,9 +1364,12 @@ struct WqRay {
   f3 oi;       // RN(o * inv) per axis
   float sig;   // 2^-23 max |o * inv|: covers the rounding of oi in each slab distance
   float R, abs_t;
+  float tau, c0;  // the scene's grazing-band width tau_g and its tau-free margin part (cone-scaled margins)
 };
-__device__ __forceinline__ WqRay wq_ray(f3 o, f3 d, f3 inv, float R, float abs_t) {
+__device__ __forceinline__ WqRay wq_ray(f3 o, f3 d, f3 inv, float R, float abs_t, float tau, float c0) {
   WqRay q;
+  q.tau = tau;
+  q.c0 = c0;
   q.o = o;
   q.d = d;
   q.inv = inv;
@@ -1398,7 +1404,21 @@ __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& 
                 fz = fmaxf(q.o.z - N0.z, N1.z - q.o.z);
     Rm = fminf(__builtin_amdgcn_sqrtf(__builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx))) * 1.0001f, q.R);
   }
+#if HRT_WQ_CONE_MARGIN
+  // Cone-scaled margin.  The host's margin a + b R assumes the worst front-facing triangle below has
+  // -d.n^ = tau_g (DESIGN.md "BVH cull": its tau-dependent part ~ 1 / (tau - rho - 4e-7)).  The member's
+  // normal cone bounds d.n^ <= fmax for every triangle below ((x + axis error) cos - the axis rounded,
+  // cos rounded down, sin up: an upper bound whenever it is negative; if the cone can contain d's
+  // direction the bound is >= 0 and unused), so when tau_e = -fmax > tau_g every front triangle has
+  // -d.n^ >= tau_e and its margin shrinks by tau_g / tau_e: mg = c0 + s (a + b R), c0 >= the tau-free
+  // part (12 eps ext + 4 eps coord) of every node's a, s = tau_g / tau_e rounded up.  Band triangles
+  // (-d.n^ < tau_g) are the band lists', back-facing ones are never accepted.
+  const float fmax = __builtin_fmaf(x + kWqAxisErr, half_hi(w9), s_up * half_lo(w10)) + 1e-6f;
+  const float sc = (-fmax > q.tau) ? fminf(1.0f, q.tau * __builtin_amdgcn_rcpf(-fmax) * 1.000002f) : 1.0f;
+  const float mg = __builtin_fmaf(sc, __builtin_fmaf(N1.w, Rm, N0.w), q.c0);
+#else
   const float mg = __builtin_fmaf(N1.w, Rm, N0.w);
+#endif
   const float tx0 = __builtin_fmaf(N0.x - mg, q.inv.x, -q.oi.x), tx1 = __builtin_fmaf(N1.x + mg, q.inv.x, -q.oi.x);
   const float ty0 = __builtin_fmaf(N0.y - mg, q.inv.y, -q.oi.y), ty1 = __builtin_fmaf(N1.y + mg, q.inv.y, -q.oi.y);
   const float tz0 = __builtin_fmaf(N0.z - mg, q.inv.z, -q.oi.z), tz1 = __builtin_fmaf(N1.z + mg, q.inv.z, -q.oi.z);
@@ -1463,7 +1483,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   // the batch's constants, read here (kargs): live for the batch only
   const KArgs K = kargs();
   const float4* prims = K->bvh_prims;
-  const float rel_t = K->bvh_rel_t, abs_coef = K->bvh_abs_coef;
+  const float rel_t = K->bvh_rel_t, abs_coef = K->bvh_abs_coef, tau_g = K->bvh_band_tau, margin_c0 = K->bvh_margin_c0;
   const uint32_t tcap = K->wq_tcap;
   spheres_first(sc, pc, sec, o, d, c);
   const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // the meshes' AABB tests and the traversal
@@ -1628,7 +1648,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const f3 rinv = shfl3(inv, r);
     const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
     const bool overflow = nc + width * nn > wq.ncap;  // wave-uniform
-    const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs);
+    const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs, tau_g, margin_c0);
     uint32_t pe[kWqSlots], li[kWqSlots];
     float pk[kWqSlots];
 #pragma unroll
