@@ -212,6 +212,7 @@ void free_scene(hrt_context* ctx, SceneBufs& s, bool keep_rays) {
   free_dev(ctx, s.bvh_irregular);
   free_dev(ctx, s.bvh_band_off);
   free_dev(ctx, s.bvh_band);
+  free_dev(ctx, s.bvh_band_nhat);
   free_dev(ctx, s.bvh_entries);
   free_dev(ctx, s.bvh_keybase);
   for (int l = 0; l < kLanes; ++l) {
@@ -468,6 +469,13 @@ hrt_status alloc_upload(hrt_context* ctx, SceneAlloc& alloc, void** dst, const v
   return bytes ? stage_upload(ctx, *dst, src, bytes) : HRT_OK;
 }
 
+// The band lists' 16-bit image, padded to whole dwords (hrt_kernels.hip band_entry reads dwords).
+std::vector<uint16_t> band16(const std::vector<uint32_t>& list) {
+  std::vector<uint16_t> v(list.begin(), list.end());
+  v.resize((v.size() + 1) & ~(size_t)1, 0);
+  return v;
+}
+
 // Fills s with a complete device copy of the scene (everything but the kept rays).
 hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays, uint32_t n_rays, bool keep_rays,
                        const hrt_sphere* spheres, uint32_t n_spheres, const hrt_triangle* tris, uint32_t n_tris,
@@ -521,7 +529,9 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
     if ((st = up(s.bvh_prims, bvh.prims, "bvh prims")) != HRT_OK ||
         (st = up(s.bvh_irregular, bvh.irregular, "bvh irregular")) != HRT_OK ||
         (st = up(s.bvh_band_off, bvh.band_off, "band offsets")) != HRT_OK ||
-        (st = up(s.bvh_band, bvh.band_list, "band lists")) != HRT_OK ||  // 8 B entries
+        (st = bvh.band_wide() ? up(s.bvh_band, bvh.band_list, "band lists")
+                              : up(s.bvh_band, band16(bvh.band_list), "band lists")) != HRT_OK ||
+        (st = up(s.bvh_band_nhat, bvh.band_nhat, "band normals")) != HRT_OK ||
         (st = up(s.bvh_entries, bvh.entries, "bvh entries")) != HRT_OK ||
         (st = up(s.bvh_keybase, bvh.key_base, "bvh key bases")) != HRT_OK)
       return st;
@@ -531,12 +541,18 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   s.bvh_info[HRT_SCENE_BVH_IRREGULAR] = bvh.n_irregular;
   s.bvh_info[HRT_SCENE_BVH_NEVER] = bvh.n_never;
   s.bvh_info[HRT_SCENE_BVH_BUILT] = built ? 1u : 0u;
-  s.bvh_info[HRT_SCENE_BVH_BAND_ENTRIES] = (uint32_t)(bvh.band_list.size() / 2);
+  s.bvh_info[HRT_SCENE_BVH_BAND_ENTRIES] = (uint32_t)bvh.band_list.size();
+  s.bvh_band_wide = bvh.band_wide() ? 1u : 0u;
+  {
+    uint32_t longest = 0;
+    for (size_t c = 0; c + 1 < bvh.band_off.size(); ++c) longest = std::max(longest, bvh.band_off[c + 1] - bvh.band_off[c]);
+    s.bvh_band_bits = 0;
+    while (s.bvh_band_bits < 32 && (longest >> s.bvh_band_bits)) ++s.bvh_band_bits;
+  }
   s.bvh_info[HRT_SCENE_BVH_SAH_MILLI] = (uint32_t)std::min(1e9, bvh.sah_tri_frac * 1000.0 + 0.5);
   s.bvh_info[HRT_SCENE_BVH_MARGIN_MILLI] = (uint32_t)std::min(1e9, margin_frac * 1000.0 + 0.5);
   s.bvh_abs_coef = bvh.abs_coef;
   s.bvh_band_tau = built ? bvh.band_tau : hrt::kBandTau;
-  s.bvh_margin_c0 = bvh.margin_c0;
   s.bvh_rel_t = bvh.rel_t;
   s.bvh_dir_res = bvh.dir_res;
   s.bvh_built_leaf = std::max(1u, std::min(leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
@@ -651,6 +667,9 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.bvh_dir_res = s.bvh_dir_res;
   p.bvh_sah_milli = s.bvh_info[HRT_SCENE_BVH_SAH_MILLI];
   p.bvh_band = s.bvh_band;
+  p.bvh_band_nhat = s.bvh_band_nhat;
+  p.bvh_band_wide = s.bvh_band_wide;
+  p.bvh_band_bits = s.bvh_band_bits;
   p.bvh_entries = s.bvh_entries;
   p.bvh_keybase = s.bvh_keybase;
   p.bvh_n_prims = s.bvh_info[HRT_SCENE_BVH_PRIMS];
@@ -659,7 +678,6 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.bvh_abs_coef = s.bvh_abs_coef;
   p.bvh_rel_t = s.bvh_rel_t;
   p.bvh_band_tau = s.bvh_band_tau;
-  p.bvh_margin_c0 = s.bvh_margin_c0;
   p.bvh_node_r = ctx->wq_node_radius == 2 ||
                  (ctx->wq_node_radius == 0 && s.bvh_info[HRT_SCENE_BVH_MARGIN_MILLI] > hrt::kNodeRadiusMarginMilli);
   p.bvh_n_irregular = s.bvh_info[HRT_SCENE_BVH_IRREGULAR];

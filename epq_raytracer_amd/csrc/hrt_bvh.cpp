@@ -410,24 +410,14 @@ void build_band_lists(BvhHost& out) {
   worker();
   for (auto& th : pool) th.join();
   for (int c = 0; c < kDirCells; ++c) out.band_off[c + 1] = out.band_off[c] + (uint32_t)lists[c].size();
-  // 8 B per entry: the prim index and n / |n| in fixed point (hrt_bvh.h kBand*): the kernel's pre-check
-  // of d.n^ against the band, widened by the quantization error (encoded once per prim)
-  std::vector<uint32_t> enc((size_t)out.n_prims * 2);
+  // entries: the prim index (hrt_bvh.h); the pre-check's normals, one per prim
+  out.band_list.resize(out.band_off[kDirCells]);
+  for (int c = 0; c < kDirCells; ++c) std::copy(lists[c].begin(), lists[c].end(), out.band_list.begin() + out.band_off[c]);
+  out.band_nhat.assign((size_t)out.n_prims * 4, 0.0f);
   for (uint32_t k = 0; k < out.n_prims; ++k) {
-    const float* n = &out.prims[(size_t)k * 16 + 12];
-    const double inv = 1.0 / norm(ld(n));
-    const int32_t qx = (int32_t)std::lround(n[0] * inv * kBandQx), qy = (int32_t)std::lround(n[1] * inv * kBandQyz),
-                  qz = (int32_t)std::lround(n[2] * inv * kBandQyz);
-    enc[2 * k] = k | ((uint32_t)qx & 0x3FFFu) << 18;
-    enc[2 * k + 1] = ((uint32_t)qy & 0xFFFFu) | ((uint32_t)qz & 0xFFFFu) << 16;
-  }
-  out.band_list.resize((size_t)out.band_off[kDirCells] * 2);
-  for (int c = 0; c < kDirCells; ++c) {
-    uint32_t* w = out.band_list.data() + (size_t)out.band_off[c] * 2;
-    for (uint32_t k : lists[c]) {
-      *w++ = enc[2 * k];
-      *w++ = enc[2 * k + 1];
-    }
+    out.band_nhat[(size_t)k * 4] = (float)nh[k].x;
+    out.band_nhat[(size_t)k * 4 + 1] = (float)nh[k].y;
+    out.band_nhat[(size_t)k * 4 + 2] = (float)nh[k].z;
   }
 }
 
@@ -638,14 +628,6 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
       msum += ((double)r[3] + (double)r[7] * R) / ext;
     }
     out.margin_frac = out.n_nodes ? msum / out.n_nodes : 0.0;
-    // the tau-free part of a node margin (2.02 x 6 eps x ext_i + 4 eps x the box's largest coordinate),
-    // bounded over the scene: the kernel's cone-scaled margin adds it unscaled
-    double ext_max = 0.0;
-    for (const Entry& en : entries) ext_max = std::max(ext_max, en.ext);
-    const double coord_max = std::max({std::fabs((double)r0[0]), std::fabs((double)r0[1]), std::fabs((double)r0[2]),
-                                       std::fabs((double)r0[4]), std::fabs((double)r0[5]), std::fabs((double)r0[6])});
-    const double eps = 5.9604644775390625e-08;
-    out.margin_c0 = round_up((2.02 * 6 * eps * ext_max + 4 * eps * coord_max) * 1.01);
   }
   out.dir_res = (uint32_t)dir_res_for(out.n_prims);
   build_band_lists(out);
@@ -672,7 +654,7 @@ extern "C" int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, co
   counts[2] = b.n_irregular;
   counts[3] = b.n_never;
   counts[4] = built ? 1u : 0u;
-  counts[5] = (uint32_t)(b.band_list.size() / 2);
+  counts[5] = (uint32_t)b.band_list.size();
   counts[6] = b.dir_res;
   if (!built) return 0;
   auto copy = [](auto* dst, uint64_t cap, const auto& v) {

@@ -42,7 +42,9 @@ struct BvhHost {
   uint32_t dir_res = 64;            // direction cells per face edge (dir_res_for)
   double sah_tri_frac = 0.0;        // expected leaf triangle tests of a uniform random ray / entries
   double margin_frac = 0.0;         // mean over nodes of (a + b R_scene) / the box's largest extent
-  std::vector<uint32_t> band_list;  // 2 words per entry: prim | n^x << 18, n^y | n^z << 16 (kBand*)
+  std::vector<uint32_t> band_list;  // per entry: its prim's index (uploaded as 16-bit words, band_wide())
+  std::vector<float> band_nhat;     // per prim: n / |n| in binary32, 0 (the entries' pre-check normal)
+  bool band_wide() const { return n_prims > 65536u; }  // entries of 32 bits instead of 16
   std::vector<float> wq_nodes;      // BUNDLE_WQ's 48 B node image (make_wq_nodes)
   bool wq_ok = false;               // the image exists (fewer than 65536 nodes)
   uint32_t wq_n_nodes = 0;          // its nodes (the binary nodes a group collapse keeps)
@@ -51,7 +53,6 @@ struct BvhHost {
   double rho_max = 0.0;
   float abs_coef = 0.0f, rel_t = 0.0f;  // box-test t-slack: [-abs_coef R, best (1 + rel_t) + abs_coef R]
   float band_tau = 0.0f;            // the grazing band's width tau_g this hierarchy was built for
-  float margin_c0 = 0.0f;           // >= every node's tau-free margin part: 12.12 eps ext_i + 4 eps coord
 };
 
 // auto HRT_OPT_WQ_NODE_RADIUS: per-node R above this HRT_SCENE_BVH_MARGIN_MILLI (island 26 / island@4 69:
@@ -66,12 +67,11 @@ constexpr float kBandTau = HRT_BAND_TAU;
 // r03: with per-triangle margins 4.5e-3 is best on cave as well -- 4.5e-3 / 6e-3 / 9e-3: 6.36 / 6.43 /
 // 6.62 ms per frame, profiles/r03/r03f_*; build_bvh takes it as a parameter, the kernels read it from
 // TraceParams::bvh_band_tau.)
-// Grazing-band entries (8 B): prim index (18 bits, kBvhMaxEntries) | round(n^x * kBandQx) as a signed
-// 14-bit field << 18; round(n^y * kBandQyz) | round(n^z * kBandQyz) << 16, signed 16-bit fields.
-// |n^ - decoded| <= 0.5 / kBandQx in x, 0.5 / kBandQyz in y, z: |d.n^ - d.decoded| <= 6.2e-5 for |d| = 1,
-// and the kernels widen their pre-check window by kBandQErr.
-constexpr float kBandQx = 8191.0f, kBandQyz = 32767.0f;
-constexpr float kBandQErr = 7e-5f;
+// Grazing-band entries: the prim index alone, 2 B (4 B above 65536 prims); the pre-check reads the
+// prim's unit normal from BvhHost::band_nhat (a few KB, cache-resident) instead of carrying a quantized
+// copy in every entry (r03: 8 B entries with fixed-point normals made the lists 29 MB on island, and
+// their reads most of the kernel's fetched bytes).  n^ in binary32 is within 2^-24 per component of
+// n / |n|, so d.n^ is off by < 4e-7 for |d| = 1, far inside the pre-check's 1e-5 widening.
 // Direction cells per cube-map face edge: finer cells mean shorter per-ray lists (a ray scans its
 // cell's list on every bounce) but ~linearly more entries per triangle (a triangle's band is a
 // great-circle strip).  256 up to 8K entries (island: 9 entries per list, 29 MB), 128 up to 32K, 64

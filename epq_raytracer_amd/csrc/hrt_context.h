@@ -52,14 +52,17 @@ struct SceneBufs {
   uint32_t* bvh_band_off = nullptr;
   uint32_t* bvh_entries = nullptr;
   uint32_t* bvh_keybase = nullptr;
-  uint2* bvh_band = nullptr;  // grazing-band entries, 8 B (hrt_bvh.h kBand*)
+  void* bvh_band = nullptr;          // grazing-band entries: prim indices, 2 B (4 B when bvh_band_wide)
+  float4* bvh_band_nhat = nullptr;   // per prim: n^ (the entries' pre-check)
+  uint32_t bvh_band_wide = 0;
+  uint32_t bvh_band_bits = 0;        // bit width of the longest band list
   // per trace lane: compacted camera-facing records of the frame (camera_lists)
   uint32_t* cam_meta[kLanes] = {};  // cam_start[n_meshes], cam_count[n_meshes]
   float4* cam_tris[kLanes] = {};    // 64 B each
   float4* cam_cull[kLanes] = {};    // 80 B each
   uint32_t n_spheres = 0, n_tris = 0, n_meshes = 0, cam_capacity = 0;
   uint32_t bvh_info[HRT_NUM_SCENE_INFO] = {};  // hrt_get_scene_info
-  float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f, bvh_band_tau = 0.0f, bvh_margin_c0 = 0.0f;
+  float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f, bvh_band_tau = 0.0f;
   uint32_t bvh_built_leaf = 4, bvh_dir_res = 64;
   uint32_t bvh_wq_n = 0, bvh_wq_width = 2;  // BUNDLE_WQ image: nodes, largest group
 };

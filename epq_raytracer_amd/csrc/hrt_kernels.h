@@ -58,7 +58,10 @@ struct TraceParams {
   const uint32_t* bvh_band_off;  // 6 bvh_dir_res^2 + 1 offsets: grazing-band prims per direction cell
   uint32_t bvh_dir_res;          // direction cells per cube-map face edge
   uint32_t bvh_sah_milli;        // hierarchy quality (HRT_SCENE_BVH_SAH_MILLI)
-  const uint2* bvh_band;         // 8 B per entry (hrt_bvh.h kBand*): prim index, quantized n^
+  const void* bvh_band;          // grazing-band entries: prim indices, 16-bit (32-bit when bvh_band_wide)
+  const float4* bvh_band_nhat;   // per prim: its unit normal (the entries' pre-check)
+  uint32_t bvh_band_wide;
+  uint32_t bvh_band_bits;        // bit width of the longest band list
   const uint32_t* bvh_entries;   // per leaf prim: triangle index | mesh << 26 (BUNDLE_BVH_LDS)
   const uint32_t* bvh_keybase;   // per mesh: key = keybase[m] + triangle index
   uint32_t bvh_n_nodes, bvh_n_irregular, bvh_n_prims, bvh_n_meshes;
@@ -71,7 +74,6 @@ struct TraceParams {
   size_t frame_stride;
   uint32_t bvh_node_r;  // BUNDLE_WQ: trace_bundle_wq_nr, box margins with a per-node R (HRT_OPT_WQ_NODE_RADIUS)
   float bvh_band_tau;   // the grazing band's width tau_g the hierarchy and band lists were built for
-  float bvh_margin_c0;  // >= the tau-free part of every node's margin a (BUNDLE_WQ cone-scaled margins)
 };
 
 // Per device, once: the dynamic-LDS limits of the persistent kernels (hipFuncSetAttribute).

@@ -815,10 +815,13 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
     }
   }
   float best_k = c.t * kOnePlus;
-  const kfloat* ct = to_const(P.cam_tris);
+  const kfloat* ct = to_const(HRT_SHADE_KARGS ? kargs()->cam_tris : P.cam_tris);
+  auto entry = [&](uint32_t i) {
+    return tl.lds ? __builtin_amdgcn_readfirstlane(tl.lds[i]) : (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
+  };
+  // (r03: requesting the next entry's record before this one's test was slower, island 2.259 -> 2.338)
   for (uint32_t i = 0; i < tl.n; ++i) {
-    const uint32_t e = tl.lds ? __builtin_amdgcn_readfirstlane(tl.lds[i])
-                              : (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
+    const uint32_t e = entry(i);
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
     const bool pass = prim && ((pm >> (8 * m)) & 1ull);
     if (!__any(pass)) continue;
@@ -1158,21 +1161,24 @@ __device__ __forceinline__ uint32_t dir_cell(f3 d, uint32_t res) {
   return (face * res + (uint32_t)iu) * res + (uint32_t)iv;
 }
 
-// Grazing-band pre-check (hrt_bvh.h kBand*): d.n^ of an 8 B entry, with d pre-scaled by the fixed-point
-// steps (ds = d / (kBandQx, kBandQyz, kBandQyz)); the window is widened by kBandQErr.
+// Grazing-band pre-check: d.n^ of an entry's prim (its unit normal from TraceParams::bvh_band_nhat)
+// inside the window (hrt_bvh.h "Grazing-band entries").
 struct BandCheck {
-  f3 ds;
+  f3 d;
   float lo, hi;
-  __device__ __forceinline__ explicit BandCheck(f3 d, float lo0, float hi0)
-      : ds(mk(d.x / kBandQx, d.y / kBandQyz, d.z / kBandQyz)), lo(lo0 - kBandQErr), hi(hi0 + kBandQErr) {}
-  __device__ __forceinline__ bool in(uint2 e) const {
-    const float qx = (float)__builtin_amdgcn_sbfe((int)e.x, 18, 14);
-    const float qy = (float)__builtin_amdgcn_sbfe((int)e.y, 0, 16), qz = (float)__builtin_amdgcn_sbfe((int)e.y, 16, 16);
-    const float dn = ds.x * qx + ds.y * qy + ds.z * qz;
+  __device__ __forceinline__ explicit BandCheck(f3 d0, float lo0, float hi0) : d(d0), lo(lo0), hi(hi0) {}
+  __device__ __forceinline__ bool in(const float4& nh) const {
+    const float dn = __builtin_fmaf(d.z, nh.z, __builtin_fmaf(d.y, nh.y, d.x * nh.x));
     return dn > lo && dn < hi;
   }
-  __device__ __forceinline__ static uint32_t prim(uint2 e) { return e.x & 0x3FFFFu; }
 };
+// Entry k of the band lists: its prim index (16-bit words unless the scene has more than 65536 prims;
+// the 16-bit array is padded to whole dwords).  One dword load either way, no branch on the width (a
+// branch between a round's loads makes the normal's wait drain the next round's entry load too).
+__device__ __forceinline__ uint32_t band_entry(const void* band, uint32_t wide, uint32_t k) {
+  const uint32_t w = static_cast<const uint32_t*>(band)[wide ? k : k >> 1];
+  return wide ? w : (w >> ((k & 1u) << 4)) & 0xFFFFu;
+}
 
 // Bounce segments through the hierarchy.  Called with ALL 64 lanes active (spheres and the
 // irregular list are wave-uniform loops; the traversal and the band list are per lane).
@@ -1211,24 +1217,29 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
   if (sec && mask) {
     const uint32_t cell = dir_cell(d, P.bvh_dir_res);
     const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
-    // Pre-check: an entry whose decoded d.n^ is outside (-tau_g - 2e-5, 3e-5) widened by the
-    // quantization error is not in this lane's band (-tau_g - 1e-5, 2e-5).
+    // Pre-check: an entry whose d.n^ is outside (-tau_g - 2e-5, 3e-5) is not in this lane's band
+    // (-tau_g - 1e-5, 2e-5).
     const BandCheck bc(d, -P.bvh_band_tau - 2e-5f, 3e-5f);
     uint32_t k = b0;
     for (; k + 4 <= b1; k += 4) {
-      const uint2 qs[4] = {P.bvh_band[k], P.bvh_band[k + 1], P.bvh_band[k + 2], P.bvh_band[k + 3]};
+      uint32_t qs[4];
+      float4 nh[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qs[j] = band_entry(P.bvh_band, P.bvh_band_wide, k + j);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nh[j] = P.bvh_band_nhat[qs[j]];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (bc.in(qs[j])) {
-          bvh.prim(BandCheck::prim(qs[j]), mask, o, d, c, bkey, best_k);
+        if (bc.in(nh[j])) {
+          bvh.prim(qs[j], mask, o, d, c, bkey, best_k);
           ++band_tests;
         }
       }
     }
     for (; k < b1; ++k) {
-      const uint2 q = P.bvh_band[k];
-      if (bc.in(q)) {
-        bvh.prim(BandCheck::prim(q), mask, o, d, c, bkey, best_k);
+      const uint32_t q = band_entry(P.bvh_band, P.bvh_band_wide, k);
+      if (bc.in(P.bvh_band_nhat[q])) {
+        bvh.prim(q, mask, o, d, c, bkey, best_k);
         ++band_tests;
       }
     }
@@ -1279,17 +1290,11 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 // hold key 0 and win ties, as they are scanned first).  A child is dropped only by BUNDLE_BVH's exact
 // node test (wq_node_visit) against the slot's current t, which only ever exceeds the final one.
 // When the node stack could overflow, the popped groups' subtrees are walked stacklessly instead.
-#ifndef HRT_WQ_CONE_MARGIN
-#define HRT_WQ_CONE_MARGIN 1  // node margins scaled by the normal cone's bound on -d.n^ (wq_member_visit)
-#endif
 #ifndef HRT_WQ_CONE
 #define HRT_WQ_CONE 1    // the nodes' back-face (normal cone) test
 #endif
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
-#endif
-#ifndef HRT_WQ_BAND_CHUNK
-#define HRT_WQ_BAND_CHUNK 1  // band rounds whose loads are issued together (2 / 4 / 8 measured slower: r02t)
 #endif
 #ifndef HRT_WQ_TRI_MIN
 #define HRT_WQ_TRI_MIN 64u  // a triangle step runs once this many triangle pairs wait (or no node pair is left)
@@ -1364,12 +1369,9 @@ struct WqRay {
   f3 oi;       // RN(o * inv) per axis
   float sig;   // 2^-23 max |o * inv|: covers the rounding of oi in each slab distance
   float R, abs_t;
-  float tau, c0;  // the scene's grazing-band width tau_g and its tau-free margin part (cone-scaled margins)
 };
-__device__ __forceinline__ WqRay wq_ray(f3 o, f3 d, f3 inv, float R, float abs_t, float tau, float c0) {
+__device__ __forceinline__ WqRay wq_ray(f3 o, f3 d, f3 inv, float R, float abs_t) {
   WqRay q;
-  q.tau = tau;
-  q.c0 = c0;
   q.o = o;
   q.d = d;
   q.inv = inv;
@@ -1404,21 +1406,9 @@ __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& 
                 fz = fmaxf(q.o.z - N0.z, N1.z - q.o.z);
     Rm = fminf(__builtin_amdgcn_sqrtf(__builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx))) * 1.0001f, q.R);
   }
-#if HRT_WQ_CONE_MARGIN
-  // Cone-scaled margin.  The host's margin a + b R assumes the worst front-facing triangle below has
-  // -d.n^ = tau_g (DESIGN.md "BVH cull": its tau-dependent part ~ 1 / (tau - rho - 4e-7)).  The member's
-  // normal cone bounds d.n^ <= fmax for every triangle below ((x + axis error) cos - the axis rounded,
-  // cos rounded down, sin up: an upper bound whenever it is negative; if the cone can contain d's
-  // direction the bound is >= 0 and unused), so when tau_e = -fmax > tau_g every front triangle has
-  // -d.n^ >= tau_e and its margin shrinks by tau_g / tau_e: mg = c0 + s (a + b R), c0 >= the tau-free
-  // part (12 eps ext + 4 eps coord) of every node's a, s = tau_g / tau_e rounded up.  Band triangles
-  // (-d.n^ < tau_g) are the band lists', back-facing ones are never accepted.
-  const float fmax = __builtin_fmaf(x + kWqAxisErr, half_hi(w9), s_up * half_lo(w10)) + 1e-6f;
-  const float sc = (-fmax > q.tau) ? fminf(1.0f, q.tau * __builtin_amdgcn_rcpf(-fmax) * 1.000002f) : 1.0f;
-  const float mg = __builtin_fmaf(sc, __builtin_fmaf(N1.w, Rm, N0.w), q.c0);
-#else
+  // (Cone-scaled margins -- c0 + (a + b R) tau_g / tau_e when the member's normal cone bounds -d.n^ >= tau_e
+  // > tau_g -- measured slower: cave 6.37 -> 6.60, island 2.25 -> 2.30 ms, profiles/r03/r03g_cone_margin_ab.)
   const float mg = __builtin_fmaf(N1.w, Rm, N0.w);
-#endif
   const float tx0 = __builtin_fmaf(N0.x - mg, q.inv.x, -q.oi.x), tx1 = __builtin_fmaf(N1.x + mg, q.inv.x, -q.oi.x);
   const float ty0 = __builtin_fmaf(N0.y - mg, q.inv.y, -q.oi.y), ty1 = __builtin_fmaf(N1.y + mg, q.inv.y, -q.oi.y);
   const float tz0 = __builtin_fmaf(N0.z - mg, q.inv.z, -q.oi.z), tz1 = __builtin_fmaf(N1.z + mg, q.inv.z, -q.oi.z);
@@ -1483,7 +1473,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   // the batch's constants, read here (kargs): live for the batch only
   const KArgs K = kargs();
   const float4* prims = K->bvh_prims;
-  const float rel_t = K->bvh_rel_t, abs_coef = K->bvh_abs_coef, tau_g = K->bvh_band_tau, margin_c0 = K->bvh_margin_c0;
+  const float rel_t = K->bvh_rel_t, abs_coef = K->bvh_abs_coef;
   const uint32_t tcap = K->wq_tcap;
   spheres_first(sc, pc, sec, o, d, c);
   const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // the meshes' AABB tests and the traversal
@@ -1531,12 +1521,17 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   // Grazing band, flattened over the wave: the bounce lanes' direction-cell lists laid end to end
   // (exclusive prefix pos of their lengths), 64 entries per round whatever the lists' lengths (the
   // per-lane scan ran as long as the batch's longest list: 33 entries against 9.3 per lane on
-  // island).  Slot g's list is the last lane with pos <= g (a binary search over the lanes); an entry
-  // that passes its ray's pre-check becomes a (ray, prim) pair of the triangle steps, whose slot
-  // minimum is the per-lane scan's result.
+  // island).  Slot g's list is the last lane with pos <= g; an entry that passes its ray's pre-check
+  // becomes a (ray, prim) pair of the triangle steps, whose slot minimum is the per-lane scan's result.
+  // r03: the scan is a chain of latencies, not VALU (without it -- wrong frames -- island 2.26 -> 1.99,
+  // cave 6.41 -> 5.42 ms): 2-byte entries with the prims' normals in a table (fetched bytes 1.08 ->
+  // 0.36 GB per island frame), rounds pipelined one ahead, ballot prefix and start marks instead of
+  // 6-step shuffle scans and binary searches: island 2.257 -> 2.154, cave 6.411 -> 6.066 ms
+  // (profiles/r03/r03i..r03l; a two-stage pipeline and offsets requested at the bounce's start were
+  // no faster).
   if (__any(sec && mask)) {
-    uint32_t b0 = 0, n = 0;
     const BandCheck bc(d, -K->bvh_band_tau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
+    uint32_t b0 = 0, n = 0;
     if (sec && mask) {
       const uint32_t* band_off = K->bvh_band_off;
       const uint32_t cell = dir_cell(d, K->bvh_dir_res);
@@ -1547,49 +1542,58 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       dg.band_len += n;
       band_lmax = n;
     }
-    uint32_t pos = n;  // inclusive prefix, then exclusive
-#pragma unroll
-    for (int sh = 1; sh < 64; sh <<= 1) {
-      const uint32_t t = (uint32_t)__shfl_up((int)pos, sh, 64);
-      if (lane >= (uint32_t)sh) pos += t;
+    // exclusive prefix pos of the lengths and their total from bit-plane ballots (no lane exchanges:
+    // bvh_band_bits = the bit width of the scene's longest list; a 6-step shuffle scan was slower)
+    uint32_t pos = 0, total = 0;
+    for (uint32_t b = 0, nb = K->bvh_band_bits; b < nb; ++b) {
+      const unsigned long long bb = __ballot((n >> b) & 1u);
+      pos += lanes_below(bb) << b;
+      total += (uint32_t)__popcll(bb) << b;
     }
-    const uint32_t total = (uint32_t)__shfl((int)pos, 63, 64);
-    pos -= n;
-    // rounds in chunks of kBandChunk: every round's owner search and entry load issued before any
-    // round's check, so the chunk waits for its (mostly L2-missing) entry loads once
-    constexpr int kBandChunk = HRT_WQ_BAND_CHUNK;
-    const uint2* band = K->bvh_band;
-    for (uint32_t base = 0; base < total; base += 64u * kBandChunk) {
-      uint32_t own[kBandChunk];
-      uint2 q[kBandChunk];
-#pragma unroll
-      for (int rr = 0; rr < kBandChunk; ++rr) {
-        const uint32_t gi = base + 64u * rr + lane;
-        uint32_t lo = 0, pl = 0;
-#pragma unroll
-        for (int st = 32; st > 0; st >>= 1) {
-          const uint32_t pm = (uint32_t)__shfl((int)pos, (int)(lo + st), 64);
-          if (pm <= gi) {
-            lo += st;
-            pl = pm;
-          }
-        }
-        own[rr] = lo;
-        const uint32_t k = (uint32_t)__shfl((int)b0, (int)lo, 64) + (gi - pl);
-        q[rr] = gi < total ? band[k] : make_uint2(0u, 0u);
-      }
-#pragma unroll
-      for (int rr = 0; rr < kBandChunk; ++rr) {
-        if (base + 64u * rr >= total) break;  // wave-uniform
-        if (tc + 64u > tcap) tri_step64();  // room for this round's pairs
-        BandCheck oc = bc;
-        oc.ds = shfl3(bc.ds, own[rr]);
-        const bool push = base + 64u * rr + lane < total && oc.in(q[rr]);
-        const unsigned long long pb = __ballot(push);
-        if (push) wq.ts[tc + lanes_below(pb)] = (BandCheck::prim(q[rr]) << 6) | own[rr];
-        tc += (uint32_t)__popcll(pb);
-        band_tests += push ? 1u : 0u;
-      }
+    const void* band = K->bvh_band;
+    const uint32_t wide = K->bvh_band_wide;
+    const float4* nhat = K->bvh_band_nhat;
+    // Round base's slot for this lane: its owner lane (the last with pos <= slot) and entry.  The
+    // lanes whose lists start in the round mark their start slot (lane + 1, one byte each, in the node
+    // stack's words: empty until the root is tested); a slot's owner is the mark at its highest marked
+    // slot at or below it, or the previous round's last owner when none is.
+    uint8_t* const marks = reinterpret_cast<uint8_t*>(wq.ns);
+    const uint32_t delta = b0 - pos;  // entry index of slot gi = delta of its owner + gi (mod 2^32)
+    uint32_t carry = 0;
+    auto fetch = [&](uint32_t base, uint32_t& own, uint32_t& q) {
+      marks[lane] = 0;
+      const uint32_t rel = pos - base;
+      if (n && rel < 64u) marks[rel] = (uint8_t)(lane + 1u);
+      const uint32_t v = marks[lane];
+      const unsigned long long m = __ballot(v != 0u) & (lane == 63u ? ~0ull : (2ull << lane) - 1ull);
+      const uint32_t s = m ? 63u - (uint32_t)__builtin_clzll(m) : 0u;
+      const uint32_t sv = (uint32_t)__shfl((int)v, (int)s, 64);
+      own = m ? sv - 1u : carry;
+      carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
+      const uint32_t gi = base + lane;
+      const uint32_t k = (uint32_t)__shfl((int)delta, (int)own, 64) + gi;
+      q = band_entry(band, wide, gi < total ? k : 0u);  // (slots past the end: entry 0, unused)
+    };
+    // Software-pipelined rounds: the next round's owner search and entry load are issued after this
+    // round's normal load and before its check, so a round waits for the (cache-resident) normal
+    // alone while the next round's (mostly L2-missing) entry load is in flight.  (The last round
+    // fetches a round past the end too: a conditional load would make the normal's wait a full drain.)
+    uint32_t own = 0, q = 0;
+    if (total) fetch(0u, own, q);
+    for (uint32_t base = 0; base < total; base += 64u) {
+      if (tc + 64u > tcap) tri_step64();  // room for this round's pairs
+      const float4 nh = nhat[q];
+      uint32_t own_n, q_n;
+      fetch(base + 64u, own_n, q_n);
+      BandCheck oc = bc;
+      oc.d = shfl3(bc.d, own);
+      const bool push = base + lane < total && oc.in(nh);
+      const unsigned long long pb = __ballot(push);
+      if (push) wq.ts[tc + lanes_below(pb)] = (q << 6) | own;
+      tc += (uint32_t)__popcll(pb);
+      band_tests += push ? 1u : 0u;
+      own = own_n;
+      q = q_n;
     }
   }
   // pair traversal: the root is tested per lane, then (ray, node group) / (ray, triangle) pairs
@@ -1648,7 +1652,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const f3 rinv = shfl3(inv, r);
     const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
     const bool overflow = nc + width * nn > wq.ncap;  // wave-uniform
-    const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs, tau_g, margin_c0);
+    const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs);
     uint32_t pe[kWqSlots], li[kWqSlots];
     float pk[kWqSlots];
 #pragma unroll

@@ -38,7 +38,7 @@ uint32_t hrt_host_ray_grid(uint32_t width, uint32_t height, float camera_focal_l
 /* Host-only inspection of the hierarchy hrt_set_scene builds for BUNDLE_BVH (tests; no GPU).
  * counts = {nodes, prims, irregular, never, built, band entries, direction cells per face edge R};
  * each array (capacity in elements: floats for nodes/prims/irregular = 16 per record, u32 for
- * band_off = 6*R*R+1 (R <= 256) and band_list = 2 per entry) is filled when non-NULL and large
+ * band_off = 6*R*R+1 (R <= 256) and band_list = 1 prim index per entry) is filled when non-NULL and large
  * enough.  Returns 1 (filled), 0 (not built), -1 (a capacity too small). */
 int hrt_debug_bvh_build(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
                         uint32_t leaf_size, uint32_t counts[7], float* nodes, uint64_t nodes_cap, float* prims,

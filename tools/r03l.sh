@@ -1,0 +1,12 @@
+#!/bin/bash
+# r03l: band rounds with bit-plane prefix and LDS start marks (scan2, + offsets hoisted: scan2h) vs the
+# binary-search owners (band2p) and the 8-byte entries (cur3); GPU suite on the product library (scan2).
+set -o pipefail
+OUT=gpurun_out/r03l; mkdir -p $OUT
+L=epq_raytracer_amd/build
+LIBS="$L/ab_cur3/libhip_raytrace.so $L/ab_band2p/libhip_raytrace.so $L/ab_scan2/libhip_raytrace.so $L/ab_scan2h/libhip_raytrace.so"
+timeout -k 10 600 bash tools/ab.sh 2 $LIBS > $OUT/ab_island.jsonl 2>&1 || { echo "ab island failed"; tail -5 $OUT/ab_island.jsonl; exit 1; }
+timeout -k 10 600 bash tools/ab.sh 2 $LIBS -- --scene cave > $OUT/ab_cave.jsonl 2>&1 || { echo "ab cave failed"; tail -5 $OUT/ab_cave.jsonl; exit 1; }
+python3 tools/ab_summary.py $OUT/ab_island.jsonl $OUT/ab_cave.jsonl
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/gpu_tests.log; exit 1; }
+tail -3 $OUT/gpu_tests.log
