@@ -600,7 +600,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   ctx->scene = s;
   ctx->debug_fail_alloc = 0;
   if (!keep_rays) ctx->n_rays = n_rays;
-  for (auto& l : ctx->lane) l.plan_valid = false;  // tile costs describe the old scene
+  for (auto& l : ctx->lane) l.plan_valid = l.cam_ready = false;  // costs and camera lists of the old scene
   ctx->scene_set = true;
   return HRT_OK;
 }
@@ -715,6 +715,12 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stre
   // lane's own image (fully overwritten by the trace that follows on the same stream) measures the
   // tiles' relative costs so that this trace already follows a plan (HRT_OPT_PROBE).
   const int resolved = hrt::resolve_variant(p, variant);
+  // camera lists: rebuilt only when the lane's were built for another position (or scene)
+  uint32_t key[4];
+  std::memcpy(key, p.pc.cam_pos, 12);
+  key[3] = p.pc.num_meshes;
+  p.cam_lists_ready = lane.cam_ready && std::memcmp(key, lane.cam_key, sizeof key) == 0 ? 1u : 0u;
+  lane.cam_ready = false;  // until a launch has rebuilt them
   if (ctx->probe && !lane.plan_valid && ctx->num_tiles() >= 1024 && persistent_kernel(resolved)) {
     hrt::TraceParams q = p;
     q.pc.num_samples = 1;
@@ -731,11 +737,16 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stre
       return hip_fail(ctx, pe, "probe trace launch");
     }
     p.plan_valid = 1u;
+    p.cam_lists_ready = 1u;  // the probe built them
   }
   HRT_HIP(ctx, hipEventRecord(ev.start, stream));
   hipError_t e = hrt::launch_trace(p, variant, stream, &ctx->last_kernel, &ctx->last_block);
   // the persistent kernels recorded this trace's tile costs: the lane's next trace can follow a plan
   lane.plan_valid = e == hipSuccess && persistent_kernel(ctx->last_kernel);
+  if (e == hipSuccess) {
+    lane.cam_ready = true;
+    std::memcpy(lane.cam_key, key, sizeof key);
+  }
   if (e != hipSuccess) {
     ctx->event_pool.push_back(ev);
     return hip_fail(ctx, e, "trace kernel launch");

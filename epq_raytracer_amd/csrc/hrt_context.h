@@ -77,6 +77,10 @@ struct Lane {
   uint32_t* tile_cost = nullptr;  // per 8x8 tile
   uint32_t* item_buf = nullptr;   // planned work items (tiles x 64)
   bool plan_valid = false;        // tile_cost describes this lane's last trace (same scene)
+  // the lane's camera lists (camera_lists) hold the records of this camera position (same scene):
+  // a trace from the same position skips rebuilding them
+  bool cam_ready = false;
+  uint32_t cam_key[4] = {};       // cam_pos bits, num_meshes
   hipEvent_t done = nullptr;      // recorded on `stream` after each trace / clear of the lane
   hipEvent_t free = nullptr;      // recorded on the context stream after the lane's last reader
   bool done_set = false, free_set = false;

@@ -62,6 +62,7 @@ struct TraceParams {
   const float4* bvh_band_nhat;   // per prim: its unit normal (the entries' pre-check)
   uint32_t bvh_band_wide;
   uint32_t bvh_band_bits;        // bit width of the longest band list
+  uint32_t cam_lists_ready;      // (host) cam_tris / cam_cull / cam_meta already hold this camera's lists
   const uint32_t* bvh_entries;   // per leaf prim: triangle index | mesh << 26 (BUNDLE_BVH_LDS)
   const uint32_t* bvh_keybase;   // per mesh: key = keybase[m] + triangle index
   uint32_t bvh_n_nodes, bvh_n_irregular, bvh_n_prims, bvh_n_meshes;

@@ -2642,7 +2642,7 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
       break;
     }
     case HRT_KERNEL_BUNDLE_BVH_LDS: {
-      if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      if (p.pc.num_meshes > 0 && !p.cam_lists_ready) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       TraceParams q = p;
       q.coop = 0;
       if (q.split_k == 0) q.split_k = 1;
@@ -2656,7 +2656,7 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
       break;
     }
     case HRT_KERNEL_BUNDLE_WQ: {
-      if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      if (p.pc.num_meshes > 0 && !p.cam_lists_ready) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       TraceParams q = p;
       q.coop = 0;
       // auto: a pair step's work scales with the rays in the batch, so heavy tiles (> factor x a
@@ -2684,7 +2684,7 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
       break;
     }
     case HRT_KERNEL_BUNDLE_CULL_LDS: {
-      if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      if (p.pc.num_meshes > 0 && !p.cam_lists_ready) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       TraceParams q = p;
       const uint32_t block = lds_block(p.n_tris);
       *block_out = (int)block;
@@ -2708,7 +2708,7 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
     case HRT_KERNEL_BUNDLE:
     case HRT_KERNEL_BUNDLE_CULL:
     case HRT_KERNEL_BUNDLE_BVH:
-      if (p.pc.num_meshes > 0) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      if (p.pc.num_meshes > 0 && !p.cam_lists_ready) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
       if (variant == HRT_KERNEL_BUNDLE)
         p.diag ? trace_bundle<true><<<grid, 256, 0, stream>>>(p) : trace_bundle<false><<<grid, 256, 0, stream>>>(p);
       else if (variant == HRT_KERNEL_BUNDLE_CULL)

@@ -367,3 +367,35 @@ def test_rng_domain_shortcuts_exhaustive():
     out = np.zeros(3, np.uint64)
     _lib.check(lib.hrt_debug_math_check_rng(0, _lib.ptr(out)), "hrt_debug_math_check_rng")
     assert out[0] == 0 and out[1] == 0 and out[2] == 0, out
+
+
+@pytest.mark.parametrize("overlap", [1, 3])
+def test_camera_lists_follow_the_camera(overlap):
+    """A lane rebuilds its camera lists (camera_lists) only when the camera position changed since its
+    last trace: a camera path A, A, B, A, B, B (across 1 or 3 trace lanes, the first trace's planning
+    probe included) gives each frame exactly the image of a fresh context traced from that position."""
+    case = SceneCase("island", (96, 64), 2, 4)
+    a = np.asarray(case.camera.position, np.float32)
+    b = a + np.float32([0.7, 0.3, -0.4])
+
+    def push(pos, k):
+        pc = case.push(k)
+        pc.cam_pos[:] = [float(pos[0]), float(pos[1]), float(pos[2]), 1.0]
+        return pc
+
+    def fresh(pos, k):
+        ctx = case.context()
+        ctx.trace(push(pos, k))
+        img = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+        ctx.close()
+        return img
+
+    path = [a, a, b, a, b, b]
+    ctx = case.context()
+    ctx.set_option(_lib.OPT_OVERLAP, overlap)
+    for k, pos in enumerate(path, start=1):
+        ctx.trace(push(pos, k))
+        got = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+        want = fresh(pos, k)
+        assert np.array_equal(got, want), f"frame {k}: {mismatch_report(got, want)}"
+    ctx.close()
