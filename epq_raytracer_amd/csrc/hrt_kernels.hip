@@ -82,6 +82,9 @@ __device__ __forceinline__ f3 get_ray_dir(const PC& pc, f3 c, uint32_t& state) {
   const float r = (u01(hash(state)) * 2.0f) * 3.14159265358979323846f;
   float sr, cr;
   spec_sincos_angle(r, sr, cr);  // r in [0, 2pi]
+  // (r03, measured slower: the zero components of t1 / t2 as signed zeros -- 4.5 M fewer VALU per
+  // frame, 2.150 -> 2.163 ms -- and the second normalize's sqrt and reciprocal from the bits of
+  // |a|^2 near 1 -- 9 M more, 2.161 ms; profiles/r03/r03p_raygen_ab.jsonl)
   const float j = pc.jitter_size;
   const float s2 = sqrt_rng(u01(hash(state)));
   const f3 t1 = ((mk(0.0f, 0.0f, 1.0f) * cr) * j) * s2;
