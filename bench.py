@@ -71,9 +71,14 @@ def parse():
                     help="after the timed steps: frames of the per-frame dispatch loop (compute_then_render) "
                          "reported as per_frame_dispatch_ms (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length (0 = skip)")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                    help="rocprofv3 PMC summary giving HBM bytes per trace launch for this workload")
-    return ap.parse_args()
+    ap.add_argument("--pmc-json", default=None,
+                    help="rocprofv3 PMC record of this build and workload (tools/pmc.sh); default "
+                         "profiles/pmc_traffic.json for island, profiles/pmc_traffic_<scene>.json otherwise")
+    a = ap.parse_args()
+    if a.pmc_json is None:
+        a.pmc_json = os.path.join(ROOT, "profiles", "pmc_traffic.json" if a.scene == "island"
+                                  else f"pmc_traffic_{a.scene}.json")
+    return a
 
 
 def resolve_launch(gpus: int, env) -> tuple:
