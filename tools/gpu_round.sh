@@ -14,7 +14,11 @@ cat $OUT/smoke.log
 fi
 bash tools/pmc.sh $TAG/pmc "$@" > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $OUT/pmc.log; exit 1; }
 cp $OUT/pmc/pmc_traffic.json $OUT/pmc_traffic.json
-timeout -k 10 600 python3 bench.py --pmc-json $OUT/pmc_traffic.json "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
+# the bench line cites the record where it is committed (profiles/<round>/<tag>_pmc/, copied there from
+# gpurun_out/<tag>/pmc_traffic.json after the call), not the scratch directory
+PMC=profiles/$(echo $TAG | cut -c1-3)/${TAG}_pmc; mkdir -p $PMC
+cp $OUT/pmc_traffic.json $PMC/pmc_traffic.json
+timeout -k 10 600 python3 bench.py --pmc-json $PMC/pmc_traffic.json "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --cpu-seconds 0 --pmc-json $OUT/pmc_traffic.json "$@" > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --cpu-seconds 0 --pmc-json $PMC/pmc_traffic.json "$@" > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
 find $OUT/prof -name '*kernel_stats.csv' -exec head -4 {} \;
