@@ -1296,6 +1296,21 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_CONE
 #define HRT_WQ_CONE 1    // the nodes' back-face (normal cone) test
 #endif
+#ifndef HRT_WQ_BRANCHLESS
+#define HRT_WQ_BRANCHLESS 1  // member test without the back-face early-out branch (r03s: island -0.6%, cave -0.3% with ALL4)
+#endif
+#ifndef HRT_WQ_ALL4
+#define HRT_WQ_ALL4 1  // all four member slots tested, masked past the group's count (r03s, with BRANCHLESS)
+#endif
+#ifndef HRT_WQ_SELECT
+#define HRT_WQ_SELECT 1  // a member's outcome as selects instead of a branch (r03t)
+#endif
+#ifndef HRT_WQ_CONE_SQ
+#define HRT_WQ_CONE_SQ 1  // the members' back-face test squared, no square root (r03t)
+#endif
+#ifndef HRT_WQ_FMA_SLACK
+#define HRT_WQ_FMA_SLACK 1  // member test: slack compare and the cone's first product as fmas (r03t)
+#endif
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
 #endif
@@ -1396,11 +1411,32 @@ __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& 
                  w10 = __builtin_bit_cast(uint32_t, N2.z);
   // (fused: each rounding here is far inside the 2e-6 / 1e-6 slacks, and the host's margins carry 1e-6
   // relative headroom over one rounding of a + b R)
+#if HRT_WQ_FMA_SLACK
+  // the first product as an fma with +0 (v_fma_mix_f32 reads the binary16 operand directly)
+  const float x = __builtin_fmaf(half_lo(w9), q.d.z, __builtin_fmaf(half_hi(w8), q.d.y, __builtin_fmaf(half_lo(w8), q.d.x, 0.0f)));
+#else
   const float x = __builtin_fmaf(half_lo(w9), q.d.z, __builtin_fmaf(half_hi(w8), q.d.y, half_lo(w8) * q.d.x));
+#endif
   const float xa = fmaxf(fabsf(x) - (2e-6f + kWqAxisErr), 0.0f);
-  const float s_up = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-xa, xa, 1.0f), 0.0f)) + 1.2e-6f;
   // (the cone test pays on cave too with per-node radii: without it 7.25 -> 7.43 ms, r03c)
-  if (HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back
+#if HRT_WQ_CONE_SQ
+  // The test below squared, without the square root and only ever stricter.  It is back <=> L > s_up sin
+  // with L = (x - E) cos - 1.1e-5 and s_up = sqrt(q) + 1.2e-6 (q = max(1 - xa^2, 0); the hardware root is
+  // within 1.2e-7 of sqrt(q) on [0, 1]).  Here: L' = (x - E) cos - 1.2e-5 (its two roundings < 2.4e-7
+  // below the 1e-6 extra), and s_up^2 <= (sqrt(q) + 1.4e-6)^2 <= q + 3e-6 (sqrt(q) <= 1); the four
+  // roundings of the right-hand side (< 2.4e-7 relative) inside the x1.00001.  L' > 0 and L'^2 > that
+  // imply L > s_up sin.  NaN -> not back.
+  const float q2 = fmaxf(__builtin_fmaf(-xa, xa, 1.0f), 0.0f);
+  const float sn = half_lo(w10);
+  const float L = __builtin_fmaf(x - kWqAxisErr, half_hi(w9), -1.2e-5f);
+  const bool back = HRT_WQ_CONE && L > 0.0f && L * L > ((q2 + 3e-6f) * (sn * sn)) * 1.00001f;
+#else
+  const float s_up = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-xa, xa, 1.0f), 0.0f)) + 1.2e-6f;
+  const bool back = HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f;
+#endif
+#if !HRT_WQ_BRANCHLESS
+  if (back) return false;
+#endif
   float Rm = q.R;
   if constexpr (NodeR) {  // trace_bundle_wq_nr (HRT_OPT_WQ_NODE_RADIUS)
     // R for this member: the ray origin's distance to the farthest corner of its box (every vertex
@@ -1418,7 +1454,15 @@ __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& 
   const float tn = fmaxf(fmaxf(-q.abs_t, fminf(tx0, tx1)), fmaxf(fminf(ty0, ty1), fminf(tz0, tz1)));
   const float tf = fminf(fminf(t_hi, fmaxf(tx0, tx1)), fminf(fmaxf(ty0, ty1), fmaxf(tz0, tz1)));
   t_near = tn;
+#if HRT_WQ_BRANCHLESS && HRT_WQ_FMA_SLACK
+  // the 1e-6 relative slacks as fmas (one rounding fewer each; the products' roundings were far inside
+  // the slacks either way)
+  return !back & !(__builtin_fmaf(-fabsf(tn), 1e-6f, tn) > __builtin_fmaf(fabsf(tf), 1e-6f, tf) + 2.0f * q.sig);
+#elif HRT_WQ_BRANCHLESS
+  return !back & !((tn - fabsf(tn) * 1e-6f) > (tf + fabsf(tf) * 1e-6f) + 2.0f * q.sig);  // NaN -> visit
+#else
   return !((tn - fabsf(tn) * 1e-6f) > (tf + fabsf(tf) * 1e-6f) + 2.0f * q.sig);  // NaN -> visit
+#endif
 }
 
 // Exact reference test (raytracing.glsl:213-241) of BVH leaf prim record (a, -) (e1, -) (e2, -) (n, -):
@@ -1668,10 +1712,19 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       const uint32_t g = e >> 6, fc = g & 0xFFFFu, gcnt = (g >> 16) + 1u;
       if (!overflow) {
         const float t_hi = wq_slot_t(wq, r) * (1.0f + rel_t) + rabs;
-        auto member = [&](const float4& N0, const float4& N1, const float4& N2, int k) {
+        auto member = [&](const float4& N0, const float4& N1, const float4& N2, int k, bool valid = true) {
           float tnear;
           const uint32_t inf = __builtin_bit_cast(uint32_t, N2.w);
-          if (wq_member_visit<NodeR>(N0, N1, N2, rq, t_hi, tnear)) {
+#if HRT_WQ_SELECT
+          // the outcome as selects: no branch, and the info word arrives with the record (a branch let
+          // hipcc sink its LDS read into the kept path: one more dependent round trip per member)
+          const bool vis = wq_member_visit<NodeR>(N0, N1, N2, rq, t_hi, tnear) & valid;
+          const bool leaf = (inf >> 27) != 0u;
+          li[k] = (vis & leaf) ? inf : 0u;
+          pe[k] = (vis & !leaf) ? ((inf << 6) | r) : ~0u;
+          pk[k] = (vis & !leaf) ? -tnear : -kFltMax;
+#else
+          if (wq_member_visit<NodeR>(N0, N1, N2, rq, t_hi, tnear) & valid) {
             if (inf >> 27) {
               li[k] = inf;
             } else {
@@ -1679,9 +1732,21 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
               pk[k] = -tnear;
             }
           }
+#endif
         };
         // members two at a time, both records read up front (six LDS reads in flight); every group
         // has >= 2 members, and an odd count reads its last member twice and keeps one
+#if HRT_WQ_ALL4
+        // (A/B) every slot tested, the ones past the group's count masked (no per-pair branch)
+#pragma unroll
+        for (int h = 0; h < (int)kWqSlots / 2; ++h) {
+          const float4* na = wq.nodes + 3 * (fc + min(2u * h, gcnt - 1u));
+          const float4* nb = wq.nodes + 3 * (fc + min(2u * h + 1u, gcnt - 1u));
+          const float4 A0 = na[0], A1 = na[1], A2 = na[2], B0 = nb[0], B1 = nb[1], B2 = nb[2];
+          member(A0, A1, A2, 2 * h, h == 0 || 2u * h < gcnt);
+          member(B0, B1, B2, 2 * h + 1, h == 0 || 2u * h + 1u < gcnt);
+        }
+#else
 #pragma unroll
         for (int h = 0; h < (int)kWqSlots / 2; ++h) {
           if (h == 0 || 2u * h < gcnt) {
@@ -1692,6 +1757,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
             if (h == 0 || 2u * h + 1u < gcnt) member(B0, B1, B2, 2 * h + 1);
           }
         }
+#endif
         // the nearest member in the last slot (pushed last = popped first)
 #pragma unroll
         for (int st = 1; st < (int)kWqSlots; st *= 2)

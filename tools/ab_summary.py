@@ -11,7 +11,7 @@ for path in sys.argv[1:]:
             continue
         d = json.loads(line)
         if "result" in d:
-            best[d["lib"].split("/")[-2]].append(min(d["result"]["ms"]))
+            best[d["lib"].split("/")[-2] if "lib" in d else (d["args"] or "(default)")].append(min(d["result"]["ms"]))
     print(path)
     for k, v in best.items():
-        print(f"  {k:12s} min {min(v):.3f}  per round {v}")
+        print(f"  {k:16s} min {min(v):.3f}  per round {v}")
