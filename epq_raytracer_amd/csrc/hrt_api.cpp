@@ -1169,6 +1169,26 @@ extern "C" hrt_status hrt_debug_math_check_rng(int device, uint64_t out[3]) {
   return HRT_OK;
 }
 
+// Test support: the band lists' wave flattening (hrt_kernels.hip BandFlat) on 64 given lists;
+// owner_entry[(r * 64 + l) * 2 + {0, 1}] = owner lane and entry of slot r * 64 + l, r < rounds.
+extern "C" hrt_status hrt_debug_band_flatten(int device, const uint32_t n[64], const uint32_t b0[64], uint32_t rounds,
+                                             uint32_t* owner_entry, uint32_t* total) {
+  if (!n || !b0 || !owner_entry || !total || rounds == 0 || rounds > 4096)
+    return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_debug_band_flatten: bad arguments");
+  uint32_t* d = nullptr;
+  const size_t words = 128 + (size_t)rounds * 128 + 1;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc((void**)&d, words * 4);
+  if (e == hipSuccess) e = hipMemcpy(d, n, 64 * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d + 64, b0, 64 * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hrt::launch_band_flatten_check(d, d + 64, rounds, d + 128, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(owner_entry, d + 128, (size_t)rounds * 128 * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(total, d + 128 + (size_t)rounds * 128, 4, hipMemcpyDeviceToHost);
+  if (d) (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "hrt_debug_band_flatten");
+  return HRT_OK;
+}
+
 extern "C" hrt_status hrt_debug_unmap_memory(void* ptr, uint64_t size) {
   if (hipMemUnmap(ptr, size) != hipSuccess || hipMemAddressFree(ptr, size) != hipSuccess) return HRT_ERR_HIP;
   return HRT_OK;

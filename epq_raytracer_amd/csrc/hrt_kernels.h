@@ -98,6 +98,8 @@ hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint3
                                 uint32_t local_rows, uint32_t row_tile, uint32_t parts, hipStream_t stream);
 // hrt_debug_math_check: fast division / sqrt paths vs the IEEE sequences (out[4] device counters).
 hipError_t launch_math_check(uint32_t n, uint32_t seed, unsigned long long* out, hipStream_t stream);
+hipError_t launch_band_flatten_check(const uint32_t* n, const uint32_t* b0, uint32_t rounds, uint32_t* out,
+                                     hipStream_t stream);  // BandFlat on 64 given lists
 hipError_t launch_math_check_rng(unsigned long long* out, hipStream_t stream);  // all 2^32 RNG states
 // BUNDLE_WQ's per-wave node-stack capacity for an image of n_nodes records with groups of `width` and
 // leaves of at most max_leaf triangles (0: does not fit the LDS)

@@ -1311,6 +1311,15 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_FMA_SLACK
 #define HRT_WQ_FMA_SLACK 1  // member test: slack compare and the cone's first product as fmas (r03t)
 #endif
+#ifndef HRT_WQ_LEAF_FLAT
+#define HRT_WQ_LEAF_FLAT 1  // kept leaves' triangle pairs pushed by one loop over the lane's count (r03u: island -1.3%, cave -1.7%)
+#endif
+#ifndef HRT_WQ_TRI_SELECT
+#define HRT_WQ_TRI_SELECT 0  // (A/B) the triangle pre-test's rejections as one predicate
+#endif
+#ifndef HRT_WQ_PUSH_DUMP
+#define HRT_WQ_PUSH_DUMP 0  // (A/B) inner-member pushes without a branch (non-pushing lanes store to a dump word)
+#endif
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
 #endif
@@ -1474,6 +1483,16 @@ __device__ __forceinline__ bool wq_tri_accept(const float4& A, const float4& B, 
   const f3 ao = o - mk(A.x, A.y, A.z);
   TriPre q;
   q.num_t = dot(ao, n);
+#if HRT_WQ_TRI_SELECT
+  // the three rejections as one predicate (no early-out branches: in a step of 64 different pairs they
+  // almost never skip the whole wave)
+  const float dn = dot(d, n);
+  const f3 dao = cross(ao, d);
+  q.num_u = dot(mk(C.x, C.y, C.z), dao);
+  q.num_v = dot(mk(B.x, B.y, B.z), dao);
+  q.det = -dn;
+  if (!(q.num_t > 0.0f) | !(dn < 0.0f) | pre_reject(q, best_k)) return false;
+#else
   if (!(q.num_t > 0.0f)) return false;
   const float dn = dot(d, n);
   if (!(dn < 0.0f)) return false;
@@ -1482,6 +1501,7 @@ __device__ __forceinline__ bool wq_tri_accept(const float4& A, const float4& B, 
   q.num_v = dot(mk(B.x, B.y, B.z), dao);
   q.det = -dn;
   if (pre_reject(q, best_k)) return false;
+#endif
   const float inv_det = 1.0f / q.det;
   dist = q.num_t * inv_det;
   const float u = q.num_u * inv_det;
@@ -1511,6 +1531,37 @@ __device__ __forceinline__ void wq_leaf_prim(const float4* __restrict__ pr, cons
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
+
+// The grazing-band lists of a wave's lanes laid end to end (world_hit_bounce_wq): lane l's list of n
+// entries starts at global slot pos (exclusive prefix of the lengths), total slots.  slot(base, own)
+// gives this lane's slot base + lane of a 64-slot round: its owner lane (the last with pos <= slot and a
+// non-empty list) and the owner's entry index (b0 + slot - pos; 0 past the end).  The lanes whose lists
+// start in the round mark their start slot (lane + 1, one byte each, in 64 bytes of LDS); a slot's owner
+// is the mark at its highest marked slot at or below it, or the previous round's last owner when none is
+// (carry).  All 64 lanes active.  hrt_debug_band_flatten runs it on given lists (tests/test_gpu_boundary.py).
+struct BandFlat {
+  uint8_t* marks;
+  uint32_t lane, n, pos, total, delta;  // delta = b0 - pos: entry of slot g = the owner's delta + g (mod 2^32)
+  uint32_t carry;
+  __device__ __forceinline__ uint32_t slot(uint32_t base, uint32_t& own) {
+    // (relaxed atomics: a slot's mark is another lane's store, so with plain accesses hipcc forwarded
+    // this lane's own clearing store to the load on the path where the lane marks nothing -- losing the
+    // start marks of lists that begin at the slot of a lane with no list of its own.  A wave's LDS
+    // accesses complete in program order, so no fence is needed on the hardware side.)
+    __hip_atomic_store(&marks[lane], (uint8_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const uint32_t rel = pos - base;
+    if (n && rel < 64u) __hip_atomic_store(&marks[rel], (uint8_t)(lane + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const uint32_t v = __hip_atomic_load(&marks[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const unsigned long long m = __ballot(v != 0u) & (lane == 63u ? ~0ull : (2ull << lane) - 1ull);
+    const uint32_t s = m ? 63u - (uint32_t)__builtin_clzll(m) : 0u;
+    const uint32_t sv = (uint32_t)__shfl((int)v, (int)s, 64);
+    own = m ? sv - 1u : carry;
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
+    const uint32_t gi = base + lane;
+    const uint32_t k = (uint32_t)__shfl((int)delta, (int)own, 64) + gi;
+    return gi < total ? k : 0u;
+  }
+};
 
 template <bool D, bool NodeR>
 __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const TraceParams& P, const WqLds& wq, bool sec,
@@ -1600,26 +1651,11 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const void* band = K->bvh_band;
     const uint32_t wide = K->bvh_band_wide;
     const float4* nhat = K->bvh_band_nhat;
-    // Round base's slot for this lane: its owner lane (the last with pos <= slot) and entry.  The
-    // lanes whose lists start in the round mark their start slot (lane + 1, one byte each, in the node
-    // stack's words: empty until the root is tested); a slot's owner is the mark at its highest marked
-    // slot at or below it, or the previous round's last owner when none is.
-    uint8_t* const marks = reinterpret_cast<uint8_t*>(wq.ns);
-    const uint32_t delta = b0 - pos;  // entry index of slot gi = delta of its owner + gi (mod 2^32)
-    uint32_t carry = 0;
+    uint8_t* const marks = reinterpret_cast<uint8_t*>(wq.ns);  // (the node stack's words: empty until the root is tested)
+    BandFlat bf{marks, lane, n, pos, total, b0 - pos, 0u};
     auto fetch = [&](uint32_t base, uint32_t& own, uint32_t& q) {
-      marks[lane] = 0;
-      const uint32_t rel = pos - base;
-      if (n && rel < 64u) marks[rel] = (uint8_t)(lane + 1u);
-      const uint32_t v = marks[lane];
-      const unsigned long long m = __ballot(v != 0u) & (lane == 63u ? ~0ull : (2ull << lane) - 1ull);
-      const uint32_t s = m ? 63u - (uint32_t)__builtin_clzll(m) : 0u;
-      const uint32_t sv = (uint32_t)__shfl((int)v, (int)s, 64);
-      own = m ? sv - 1u : carry;
-      carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
-      const uint32_t gi = base + lane;
-      const uint32_t k = (uint32_t)__shfl((int)delta, (int)own, 64) + gi;
-      q = band_entry(band, wide, gi < total ? k : 0u);  // (slots past the end: entry 0, unused)
+      const uint32_t k = bf.slot(base, own);
+      q = band_entry(band, wide, k);  // (slots past the end: entry 0, unused)
     };
     // Software-pipelined rounds: the next round's owner search and entry load are issued after this
     // round's normal load and before its check, so a round waits for the (cache-resident) normal
@@ -1636,7 +1672,12 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       oc.d = shfl3(bc.d, own);
       const bool push = base + lane < total && oc.in(nh);
       const unsigned long long pb = __ballot(push);
+#if HRT_WQ_PUSH_DUMP
+      // (non-pushing lanes store into the node stack's last word: empty during the band rounds)
+      (push ? wq.ts[tc + lanes_below(pb)] : wq.ns[wq.ncap - 1u]) = (q << 6) | own;
+#else
       if (push) wq.ts[tc + lanes_below(pb)] = (q << 6) | own;
+#endif
       tc += (uint32_t)__popcll(pb);
       band_tests += push ? 1u : 0u;
       own = own_n;
@@ -1698,7 +1739,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     // abs_coef * R instead of a shuffle -- island 2.271 -> 2.276, cave 7.248 -> 7.310 ms)
     const f3 rinv = shfl3(inv, r);
     const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
-    const bool overflow = nc + width * nn > wq.ncap;  // wave-uniform
+    const bool overflow = nc + width * nn > wq.ncap - (HRT_WQ_PUSH_DUMP ? 1u : 0u);  // wave-uniform
     const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs);
     uint32_t pe[kWqSlots], li[kWqSlots];
     float pk[kWqSlots];
@@ -1785,7 +1826,13 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     for (int k = 0; k < (int)kWqSlots; ++k) {
       const bool push = pe[k] != ~0u;
       const unsigned long long bk = __ballot(push);
+#if HRT_WQ_PUSH_DUMP
+      // every lane stores (no branch): the others into the stack's last word, which no entry reaches
+      // (the overflow test keeps nc + width nn below ncap)
+      wq.ns[push ? nc + lanes_below(bk) : wq.ncap - 1u] = pe[k];
+#else
       if (push) wq.ns[nc + lanes_below(bk)] = pe[k];
+#endif
       nc += (uint32_t)__popcll(bk);
     }
     // kept leaves' triangles: exclusive prefix of the per-lane counts (0..16) from bit-plane ballots
@@ -1801,12 +1848,25 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     }
     if (tc + tot <= tcap) {  // wave-uniform
       uint32_t at = tc + pre;
+#if HRT_WQ_LEAF_FLAT
+      // one loop over the lane's kept triangles (slot of entry j by its running start, selects),
+      // instead of a loop per slot
+      const uint32_t c0 = li[0] >> 27, c1 = li[1] >> 27, c2 = li[2] >> 27;
+      const uint32_t s1 = c0, s2 = s1 + c1, s3 = s2 + c2;
+      const uint32_t f0 = li[0] & 0x07FFFFFFu, f1 = (li[1] & 0x07FFFFFFu) - s1, f2 = (li[2] & 0x07FFFFFFu) - s2,
+                     f3 = (li[3] & 0x07FFFFFFu) - s3;
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const uint32_t f = j >= s3 ? f3 : j >= s2 ? f2 : j >= s1 ? f1 : f0;
+        wq.ts[at + j] = ((f + j) << 6) | r;
+      }
+#else
 #pragma unroll
       for (int k = 0; k < (int)kWqSlots; ++k) {
         const uint32_t c = li[k] >> 27, first = li[k] & 0x07FFFFFFu;
         for (uint32_t j = 0; j < c; ++j) wq.ts[at + j] = ((first + j) << 6) | r;
         at += c;
       }
+#endif
       tc += tot;
     } else {  // a burst of kept leaves beyond the triangle stack: each lane tests its own in place
 #pragma unroll
@@ -2528,6 +2588,28 @@ __global__ __launch_bounds__(256) void math_check_rng(uint32_t base, unsigned lo
   const bool bad_rcp = bk >= 0x1p-40f && bk <= 0x1p40f && fbits(rcp_core(bk)) != fbits(1.0f / bk);
   if (bad_fast || bad_log || bad_rcp) atomicAdd(&out[2], 1ull);
 }
+// hrt_debug_band_flatten: BandFlat on 64 given lists (n[l], b0[l]); out[(r * 64 + l) * 2 + {0, 1}] = the
+// owner and entry of slot r * 64 + l for each round r < rounds, and out[rounds * 128] = total.
+__global__ __launch_bounds__(64) void band_flatten_check(const uint32_t* n_in, const uint32_t* b0_in, uint32_t rounds,
+                                                         uint32_t* out) {
+  __shared__ uint8_t marks[64];
+  const uint32_t lane = threadIdx.x & 63u, n = n_in[lane], b0 = b0_in[lane];
+  uint32_t pos = 0, total = 0;
+  for (uint32_t b = 0; b < 32u; ++b) {
+    const unsigned long long bb = __ballot((n >> b) & 1u);
+    pos += lanes_below(bb) << b;
+    total += (uint32_t)__popcll(bb) << b;
+  }
+  BandFlat bf{marks, lane, n, pos, total, b0 - pos, 0u};
+  for (uint32_t r = 0; r < rounds; ++r) {
+    uint32_t own;
+    const uint32_t k = bf.slot(r * 64u, own);
+    out[(r * 64u + lane) * 2u] = own;
+    out[(r * 64u + lane) * 2u + 1u] = k;
+  }
+  if (lane == 0) out[rounds * 128u] = total;
+}
+
 __global__ __launch_bounds__(256) void math_check(uint32_t n, uint32_t seed, unsigned long long* out) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
@@ -2845,6 +2927,11 @@ hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint3
   return hipGetLastError();
 }
 
+hipError_t launch_band_flatten_check(const uint32_t* n, const uint32_t* b0, uint32_t rounds, uint32_t* out,
+                                     hipStream_t stream) {
+  band_flatten_check<<<1, 64, 0, stream>>>(n, b0, rounds, out);
+  return hipGetLastError();
+}
 hipError_t launch_math_check_rng(unsigned long long* out, hipStream_t stream) {
   for (uint64_t base = 0; base < (1ull << 32); base += (1ull << 28)) {  // 16 launches of 2^28 states
     math_check_rng<<<(1u << 28) / 256u, 256, 0, stream>>>((uint32_t)base, out);

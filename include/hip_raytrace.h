@@ -39,9 +39,10 @@
 extern "C" {
 #endif
 
-/* 2 (r03): HRT_ERR_COMM, HRT_IMG_LOCAL, HRT_OPT_COMM_TIMEOUT_MS, collective error agreement;
+/* 3 (r03): hrt_debug_band_flatten.
+ * 2 (r03): HRT_ERR_COMM, HRT_IMG_LOCAL, HRT_OPT_COMM_TIMEOUT_MS, collective error agreement;
  * hrt_debug_bvh_wq_nodes' width parameter; HRT_NUM_DIAG / HRT_NUM_SCENE_INFO grown (r02). */
-#define HRT_ABI_VERSION 2u
+#define HRT_ABI_VERSION 3u
 
 typedef enum hrt_status {
   HRT_OK = 0,
@@ -437,6 +438,12 @@ hrt_status hrt_debug_math_check(int device, uint32_t n, uint32_t seed, uint64_t 
  * RNG's angles without the range guard) against the general routines over all 2^32 states.
  * out = {sqrt mismatches, sincos mismatches, Lambertian-shortcut premise violations (hrt_kernels.hip adjust_dir)}. */
 hrt_status hrt_debug_math_check_rng(int device, uint64_t out[3]);
+/* Test support: the trace kernel's flattening of a wave's grazing-band lists (64 lanes, lane l's list
+ * of n[l] entries starting at entry b0[l]) into 64-slot rounds.  owner_entry[(r * 64 + l) * 2 + {0, 1}] =
+ * the owner lane and entry index of slot r * 64 + l (entry 0 past the end), r < rounds <= 4096;
+ * *total = the slots in all (the sum of n). */
+hrt_status hrt_debug_band_flatten(int device, const uint32_t n[64], const uint32_t b0[64], uint32_t rounds,
+                                  uint32_t* owner_entry, uint32_t* total);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
 /* The context's HIP stream (hipStream_t), for callers that interoperate: work enqueued on it after

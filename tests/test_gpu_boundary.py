@@ -369,6 +369,55 @@ def test_rng_domain_shortcuts_exhaustive():
     assert out[0] == 0 and out[1] == 0 and out[2] == 0, out
 
 
+def _band_flatten_expected(n, b0):
+    """Slot g of the lanes' lists laid end to end: (owner lane, entry) -- the last lane with a
+    non-empty list starting at or before g."""
+    pos = np.concatenate(([0], np.cumsum(n)[:-1])).astype(np.int64)
+    own, ent = [], []
+    for g in range(int(n.sum())):
+        lane = max(l for l in range(64) if n[l] and pos[l] <= g)
+        own.append(lane)
+        ent.append((int(b0[lane]) + g - int(pos[lane])) & 0xFFFFFFFF)
+    return np.array(own, np.uint32), np.array(ent, np.uint32)
+
+
+@pytest.mark.parametrize("case", ["sparse", "dense", "long", "empty_head", "one_lane", "all_empty", "random"])
+def test_band_flatten_matches_host(case):
+    """The trace kernel's flattening of a wave's grazing-band lists into 64-slot rounds (BandFlat): every
+    slot's owner lane and entry equal the host's, for lists of every shape -- in particular slots where
+    a list starts at the slot of a lane whose own list is empty (r03: a plain LDS load there let hipcc
+    forward that lane's own clearing store, so those starts were lost and their entries went to the
+    previous list's ray)."""
+    rng = np.random.default_rng(11 + ["sparse", "dense", "long", "empty_head", "one_lane", "all_empty", "random"].index(case))
+    n = np.zeros(64, np.uint32)
+    if case == "sparse":      # a bounce batch: ~40% of the lanes without a list, short lists
+        n[:] = np.where(rng.random(64) < 0.4, 0, rng.integers(1, 30, 64))
+    elif case == "dense":
+        n[:] = rng.integers(1, 5, 64)
+    elif case == "long":      # lists spanning several rounds
+        n[::7] = rng.integers(60, 200, len(n[::7]))
+    elif case == "empty_head":
+        n[20:] = rng.integers(0, 9, 44)
+    elif case == "one_lane":
+        n[63] = 150
+    elif case == "random":
+        n[:] = rng.integers(0, 40, 64) * (rng.random(64) < 0.6)
+    b0 = rng.integers(0, 1 << 20, 64).astype(np.uint32)
+    total_exp = int(n.sum())
+    rounds = max(1, -(-total_exp // 64)) + 1  # one round past the end, as the kernel's pipeline fetches
+    out = np.zeros(rounds * 128, np.uint32)
+    total = np.zeros(1, np.uint32)
+    lib = _lib.load()
+    _lib.check(lib.hrt_debug_band_flatten(0, _lib.ptr(n), _lib.ptr(b0), rounds, _lib.ptr(out), _lib.ptr(total)),
+               "hrt_debug_band_flatten")
+    assert int(total[0]) == total_exp
+    own, ent = _band_flatten_expected(n, b0)
+    got = out.reshape(-1, 2)[:total_exp]
+    bad = np.nonzero((got[:, 0] != own) | (got[:, 1] != ent))[0]
+    assert bad.size == 0, f"{bad.size} of {total_exp} slots wrong, first {bad[:5]}: got {got[bad[:3]]}, want owner {own[bad[:3]]} entry {ent[bad[:3]]}"
+    assert (out.reshape(-1, 2)[total_exp:, 1] == 0).all()  # slots past the end read entry 0
+
+
 @pytest.mark.parametrize("overlap", [1, 3])
 def test_camera_lists_follow_the_camera(overlap):
     """A lane rebuilds its camera lists (camera_lists) only when the camera position changed since its
