@@ -60,12 +60,16 @@ struct BvhHost {
 constexpr uint32_t kNodeRadiusMarginMilli = 100;
 
 #ifndef HRT_BAND_TAU
-#define HRT_BAND_TAU 4.5e-3f
+#define HRT_BAND_TAU 3e-3f
 #endif
 constexpr float kBandTau = HRT_BAND_TAU;
 // (tau_g trades the nodes' box margins, ~ 1 / tau_g, against the band lists' length, ~ cell + tau_g.
-// r03: with per-triangle margins 4.5e-3 is best on cave as well -- 4.5e-3 / 6e-3 / 9e-3: 6.36 / 6.43 /
-// 6.62 ms per frame, profiles/r03/r03f_*; build_bvh takes it as a parameter, the kernels read it from
+// r03: 4.5e-3 / 6e-3 / 9e-3: 6.36 / 6.43 / 6.62 ms per frame on cave (profiles/r03/r03f_*) -- measured
+// while the band's owner search lost list starts (fixed in r03v); with every band entry tested for its
+// own ray a band test is the dearer side: 3e-3 with 512 cells per face edge, island 2.132 -> 2.091, cave
+// 6.041 -> 5.857 ms (2e-3: 2.090 / 5.863, 1.5e-3: 2.099 / 5.865; profiles/r03/r03w_*, r03x_*).  The
+// node margins cost little (tools/margin_emul.py: 7.1 -> 7.5 leaf tests per cave bounce ray at 2e-3).
+// build_bvh takes it as a parameter, the kernels read it from
 // TraceParams::bvh_band_tau.)
 // Grazing-band entries: the prim index alone, 2 B (4 B above 65536 prims); the pre-check reads the
 // prim's unit normal from BvhHost::band_nhat (a few KB, cache-resident) instead of carrying a quantized
@@ -77,7 +81,7 @@ constexpr float kBandTau = HRT_BAND_TAU;
 // great-circle strip).  256 up to 8K entries (island: 9 entries per list, 29 MB), 128 up to 32K, 64
 // above (profiles/r01p_*).
 #ifndef HRT_DIR_RES_SMALL
-#define HRT_DIR_RES_SMALL 256
+#define HRT_DIR_RES_SMALL 512  // (r03x; 256 before)
 #endif
 constexpr int kDirResMax = HRT_DIR_RES_SMALL;
 inline int dir_res_for(uint64_t entries) { return entries <= 8192 ? HRT_DIR_RES_SMALL : entries <= 32768 ? 128 : 64; }

@@ -17,8 +17,8 @@ import pytest
 
 from helpers import E, SceneCase, _lib
 
-TAU_G = np.float32(4.5e-3)   # hrt_bvh.h kBandTau
-DIR_RES_MAX = 256          # hrt_bvh.h kDirResMax (the scene's resolution comes back in counts[6])
+TAU_G = np.float32(3e-3)     # hrt_bvh.h kBandTau
+DIR_RES_MAX = 512          # hrt_bvh.h kDirResMax (the scene's resolution comes back in counts[6])
 
 
 def build(tris, meshes, leaf=4):

@@ -27,7 +27,7 @@ P=b['prims'].astype(np.float64); N=b['nodes']
 A=P[:,0:3]; E1=P[:,4:7]; E2=P[:,8:11]; NR_=P[:,12:15]
 B=A+E1; C=A+E2
 nn=np.linalg.norm(NR_,axis=1); nh=NR_/nn[:,None]
-eps=2.0**-24; tau=4.5e-3
+eps=2.0**-24; tau=float(os.environ.get("TAU", "4.5e-3"))
 rho=np.linalg.norm(NR_-np.cross(E1,E2),axis=1)/nn+1e-12
 g=np.maximum(np.linalg.norm(E1,axis=1),np.linalg.norm(E2,axis=1))/nn
 lo=np.minimum(np.minimum(A,B),C); hi=np.maximum(np.maximum(A,B),C); ext=(hi-lo).max(1)
