@@ -66,9 +66,10 @@ constexpr float kBandTau = HRT_BAND_TAU;
 // (tau_g trades the nodes' box margins, ~ 1 / tau_g, against the band lists' length, ~ cell + tau_g.
 // r03: 4.5e-3 / 6e-3 / 9e-3: 6.36 / 6.43 / 6.62 ms per frame on cave (profiles/r03/r03f_*) -- measured
 // while the band's owner search lost list starts (fixed in r03v); with every band entry tested for its
-// own ray a band test is the dearer side: 3e-3 with 512 cells per face edge, island 2.132 -> 2.091, cave
-// 6.041 -> 5.857 ms (2e-3: 2.090 / 5.863, 1.5e-3: 2.099 / 5.865; profiles/r03/r03w_*, r03x_*).  The
-// node margins cost little (tools/margin_emul.py: 7.1 -> 7.5 leaf tests per cave bounce ray at 2e-3).
+// own ray a band test is the dearer side: 3e-3, island 2.132 -> 2.109, cave 6.041 -> 5.945 ms with 256
+// cells per face edge (512 cells: 2.089 / 5.827 ms but 3x the counter bytes, below; 2e-3 and 1.5e-3
+// measure the same; profiles/r03/r03w_*, r03x_*, r03z_*).  The node margins cost little
+// (tools/margin_emul.py: 7.1 -> 7.5 leaf tests per cave bounce ray at 2e-3).
 // build_bvh takes it as a parameter, the kernels read it from
 // TraceParams::bvh_band_tau.)
 // Grazing-band entries: the prim index alone, 2 B (4 B above 65536 prims); the pre-check reads the
@@ -81,7 +82,10 @@ constexpr float kBandTau = HRT_BAND_TAU;
 // great-circle strip).  256 up to 8K entries (island: 9 entries per list, 29 MB), 128 up to 32K, 64
 // above (profiles/r01p_*).
 #ifndef HRT_DIR_RES_SMALL
-#define HRT_DIR_RES_SMALL 512  // (r03x; 256 before)
+// r03z (tau 3e-3): 256 / 384 / 512 cells -- island 2.109 / 2.101 / 2.089 ms, FETCH_SIZE x2 0.32 / 0.76 /
+// 1.06 GB per frame; cave 5.945 / 5.871 / 5.827 ms, 0.40 / 0.64 / 0.80 GB: the finer lists are 1-2%
+// faster but no longer fit the L2 (island 512: 16.5 MB of entries + 6.3 MB of offsets), 256 kept.
+#define HRT_DIR_RES_SMALL 256
 #endif
 constexpr int kDirResMax = HRT_DIR_RES_SMALL;
 inline int dir_res_for(uint64_t entries) { return entries <= 8192 ? HRT_DIR_RES_SMALL : entries <= 32768 ? 128 : 64; }

@@ -18,7 +18,7 @@ import pytest
 from helpers import E, SceneCase, _lib
 
 TAU_G = np.float32(3e-3)     # hrt_bvh.h kBandTau
-DIR_RES_MAX = 512          # hrt_bvh.h kDirResMax (the scene's resolution comes back in counts[6])
+DIR_RES_MAX = 256          # hrt_bvh.h kDirResMax (the scene's resolution comes back in counts[6])
 
 
 def build(tris, meshes, leaf=4):
