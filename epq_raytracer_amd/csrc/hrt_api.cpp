@@ -553,6 +553,7 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   s.bvh_info[HRT_SCENE_BVH_MARGIN_MILLI] = (uint32_t)std::min(1e9, margin_frac * 1000.0 + 0.5);
   s.bvh_abs_coef = bvh.abs_coef;
   s.bvh_band_tau = built ? bvh.band_tau : hrt::kBandTau;
+  s.bvh_band_a1 = built ? bvh.band_a1 : 0.0f;
   s.bvh_rel_t = bvh.rel_t;
   s.bvh_dir_res = bvh.dir_res;
   s.bvh_built_leaf = std::max(1u, std::min(leaf, hrt::kBvhMaxLeafCount));  // leaves hold at most this
@@ -678,6 +679,7 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.bvh_abs_coef = s.bvh_abs_coef;
   p.bvh_rel_t = s.bvh_rel_t;
   p.bvh_band_tau = s.bvh_band_tau;
+  p.bvh_band_a1 = s.bvh_band_a1;
   p.bvh_node_r = ctx->wq_node_radius == 2 ||
                  (ctx->wq_node_radius == 0 && s.bvh_info[HRT_SCENE_BVH_MARGIN_MILLI] > hrt::kNodeRadiusMarginMilli);
   p.bvh_n_irregular = s.bvh_info[HRT_SCENE_BVH_IRREGULAR];

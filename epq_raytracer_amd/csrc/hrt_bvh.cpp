@@ -418,6 +418,10 @@ void build_band_lists(BvhHost& out) {
     out.band_nhat[(size_t)k * 4] = (float)nh[k].x;
     out.band_nhat[(size_t)k * 4 + 1] = (float)nh[k].y;
     out.band_nhat[(size_t)k * 4 + 2] = (float)nh[k].z;
+    // the plane's offset n^.a (the kernel's plane-side filter of band entries)
+    const V3 a = ld(&out.prims[(size_t)k * 16]);
+    out.band_nhat[(size_t)k * 4 + 3] = (float)dot(nh[k], a);
+    out.band_a1 = std::max(out.band_a1, round_up(std::fabs(a.x) + std::fabs(a.y) + std::fabs(a.z)));
   }
 }
 

@@ -43,7 +43,8 @@ struct BvhHost {
   double sah_tri_frac = 0.0;        // expected leaf triangle tests of a uniform random ray / entries
   double margin_frac = 0.0;         // mean over nodes of (a + b R_scene) / the box's largest extent
   std::vector<uint32_t> band_list;  // per entry: its prim's index (uploaded as 16-bit words, band_wide())
-  std::vector<float> band_nhat;     // per prim: n / |n| in binary32, 0 (the entries' pre-check normal)
+  std::vector<float> band_nhat;     // per prim: n / |n| in binary32, n^.a (the entries' pre-check normal and plane)
+  float band_a1 = 0.0f;             // max over prims of |a|_1 (the plane filter's tolerance)
   bool band_wide() const { return n_prims > 65536u; }  // entries of 32 bits instead of 16
   std::vector<float> wq_nodes;      // BUNDLE_WQ's 48 B node image (make_wq_nodes)
   bool wq_ok = false;               // the image exists (fewer than 65536 nodes)

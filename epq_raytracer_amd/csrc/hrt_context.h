@@ -62,7 +62,7 @@ struct SceneBufs {
   float4* cam_cull[kLanes] = {};    // 80 B each
   uint32_t n_spheres = 0, n_tris = 0, n_meshes = 0, cam_capacity = 0;
   uint32_t bvh_info[HRT_NUM_SCENE_INFO] = {};  // hrt_get_scene_info
-  float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f, bvh_band_tau = 0.0f;
+  float bvh_abs_coef = 0.0f, bvh_rel_t = 0.0f, bvh_band_tau = 0.0f, bvh_band_a1 = 0.0f;
   uint32_t bvh_built_leaf = 4, bvh_dir_res = 64;
   uint32_t bvh_wq_n = 0, bvh_wq_width = 2;  // BUNDLE_WQ image: nodes, largest group
 };

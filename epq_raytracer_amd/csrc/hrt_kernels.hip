@@ -1320,6 +1320,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_PUSH_DUMP
 #define HRT_WQ_PUSH_DUMP 0  // (A/B) inner-member pushes without a branch (non-pushing lanes store to a dump word)
 #endif
+#ifndef HRT_WQ_BAND_PLANE
+#define HRT_WQ_BAND_PLANE 1  // band entries whose plane the ray starts behind are dropped (r03aa: band tests per cave lane 3.9 -> 0.8; island -0.9%, cave -1.6%)
+#endif
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
 #endif
@@ -1629,6 +1632,14 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   // no faster).
   if (__any(sec && mask)) {
     const BandCheck bc(d, -K->bvh_band_tau - 2e-5f, 3e-5f);  // see world_hit_bounce_bvh
+#if HRT_WQ_BAND_PLANE
+    // Plane-side filter: an entry whose plane the ray starts behind, s = n^.o - n^.a < -ptol, cannot be
+    // accepted.  The reference's num_t = dot(o - a, n) is within 4 eps (|o|_1 + |a|_1) |n| of |n| times
+    // the exact n^.(o - a), and s within 6 eps (|o|_1 + |a|_1) of it (n^ within 2^-24 per component, the
+    // fma chain, the host's rounding of n^.a, the subtraction), so s < -1e-5 (|o|_1 + max |a|_1) means
+    // num_t < 0: dist <= 0, rejected (raytracing.glsl:233-238).  NaN -> kept.
+    const float ptol = 1e-5f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + K->bvh_band_a1);
+#endif
     uint32_t b0 = 0, n = 0;
     if (sec && mask) {
       const uint32_t* band_off = K->bvh_band_off;
@@ -1670,7 +1681,14 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       fetch(base + 64u, own_n, q_n);
       BandCheck oc = bc;
       oc.d = shfl3(bc.d, own);
+#if HRT_WQ_BAND_PLANE
+      const f3 oo = shfl3(o, own);
+      const float ot = __shfl(ptol, (int)own, 64);
+      const float sp = __builtin_fmaf(oo.z, nh.z, __builtin_fmaf(oo.y, nh.y, oo.x * nh.x)) - nh.w;
+      const bool push = base + lane < total && oc.in(nh) && !(sp < -ot);
+#else
       const bool push = base + lane < total && oc.in(nh);
+#endif
       const unsigned long long pb = __ballot(push);
 #if HRT_WQ_PUSH_DUMP
       // (non-pushing lanes store into the node stack's last word: empty during the band rounds)
