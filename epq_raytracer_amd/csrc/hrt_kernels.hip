@@ -207,6 +207,9 @@ __device__ __forceinline__ f3 environment_light(const hrt_push_constants& pc, f3
 #ifndef HRT_FUZZ_FAST
 #define HRT_FUZZ_FAST 1
 #endif
+#ifndef HRT_FUZZ_INT
+#define HRT_FUZZ_INT 1  // the fast path's radius test on the hash bits (r03ai)
+#endif
 __device__ __forceinline__ f3 adjust_dir(f3 d, f3 n, const hrt_material& mat, bool specular, uint32_t& state) {
   const f3 diffuse_dir = normalize(n + unit_sphere(state));
   const float k = 2.0f * dot(n, d);
@@ -227,8 +230,15 @@ __device__ __forceinline__ f3 adjust_dir(f3 d, f3 n, const hrt_material& mat, bo
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     hash(st);  // the angle's
+#if HRT_FUZZ_INT
+    // u01(h) = RN(h) 2^-32 is 0 iff h == 0 and 1 iff RN(h) == 2^32, i.e. h >= 2^32 - 128 (the u32 -> f32
+    // conversion rounds to nearest even: 2^32 - 128 is a tie between 2^32 - 256 (odd) and 2^32), so
+    // the radius test is one integer compare instead of a conversion, a multiply and two compares
+    fast &= hash(st) - 1u < 0xFFFFFF7Fu;
+#else
     const float u = u01(hash(st));
     fast &= u != 0.0f && u != 1.0f;
+#endif
   }
   const bool finite_nz = fabsf(diffuse_dir.x) < __builtin_inff() && fabsf(diffuse_dir.y) < __builtin_inff() &&
                          fabsf(diffuse_dir.z) < __builtin_inff() && diffuse_dir.x != 0.0f && diffuse_dir.y != 0.0f &&
@@ -2596,7 +2606,8 @@ __global__ __launch_bounds__(256) void math_check_rng(uint32_t base, unsigned lo
                       fbits(c2) != fbits(c3);
   const float rho = sqrt_rng(l);
   const bool rho_nz = fabsf(rho) < __builtin_inff() && rho != 0.0f;
-  const bool bad_fast = rho_nz != (u != 0.0f && u != 1.0f) || c3 == 0.0f;
+  const bool bad_fast = rho_nz != (u != 0.0f && u != 1.0f) || c3 == 0.0f ||
+                        (k - 1u < 0xFFFFFF7Fu) != (u != 0.0f && u != 1.0f);  // adjust_dir's HRT_FUZZ_INT test
   const bool bad_log = fbits(spec_log_u01(u)) != fbits(spec_log(u));
   if (bad_sqrt) atomicAdd(&out[0], 1ull);
   if (bad_sc) atomicAdd(&out[1], 1ull);
