@@ -41,6 +41,22 @@ def test_scale01_values():
         assert O.scale01(s) == float(np.float32(s)) / 2.0**32
 
 
+def test_u01_endpoint_test_on_hash_bits():
+    """adjust_dir's fast path (csrc/hrt_kernels.hip, HRT_FUZZ_INT) decides u01(h) not in {0, 1} as the
+    integer compare (h - 1) mod 2^32 < 0xFFFFFF7F: u01(h) is 0 iff h == 0 and 1 iff float_rne(h) == 2^32,
+    i.e. h >= 2^32 - 128.  Checked here on both ends of the range and a random sample (the device
+    self-check hrt_debug_math_check_rng covers all 2^32 states)."""
+    rng = np.random.default_rng(5)
+    hs = np.concatenate([np.arange(0, 1 << 20, dtype=np.uint64),
+                         np.arange((1 << 32) - (1 << 20), 1 << 32, dtype=np.uint64),
+                         rng.integers(0, 1 << 32, 1 << 20, dtype=np.uint64)]).astype(np.uint32)
+    u = hs.astype(np.float32) * np.float32(2.0 ** -32)
+    fast_float = (u != 0.0) & (u != 1.0)
+    fast_int = (hs - np.uint32(1)) < np.uint32(0xFFFFFF7F)
+    np.testing.assert_array_equal(fast_int, fast_float)
+    assert O.scale01(0xFFFFFF7F) < 1.0 and O.scale01(0xFFFFFF80) == 1.0
+
+
 def test_spec_log_accuracy_and_specials():
     rng = np.random.default_rng(1)
     xs = np.concatenate([rng.random(4000), rng.random(500) * 1e-40, [1.0, 2.0**-32, 0.5, 1e-45, 3.0, 1e30]])
