@@ -113,7 +113,7 @@ KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle"
 DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounce_iters", "bounce_considered",
               "bounce_survivors", "bounce_lanes", "bvh_visits", "bvh_prim_tests", "bvh_band_tests", "primary_cycles", "bounce_cycles",
               "shade_cycles", "bounce_stage2", "bounce_front", "bvh_trips",
-              "bvh_leaf_trips", "band_scan_max", "band_scan_len")
+              "bvh_leaf_trips", "band_scan_max", "band_scan_len", "sky_items", "sky_cycles")
 SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh_built", "bvh_band_entries",
                     "bvh_sah_milli", "bvh_margin_milli")
 

@@ -692,6 +692,11 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
 bool persistent_kernel(int k) {
   return k == HRT_KERNEL_BUNDLE_WQ || k == HRT_KERNEL_BUNDLE_CULL_LDS || k == HRT_KERNEL_BUNDLE_BVH_LDS;
 }
+// The kernels whose launch (re)builds the lane's camera lists (launch_trace runs camera_lists before
+// them); LITERAL, BRUTE and BRUTE_LDS neither build nor read the lists.
+bool builds_camera_lists(int k) {
+  return persistent_kernel(k) || k == HRT_KERNEL_BUNDLE || k == HRT_KERNEL_BUNDLE_CULL || k == HRT_KERNEL_BUNDLE_BVH;
+}
 
 // One trace launch of p.n_frames frames on `stream` with lane l's planner buffers (timed by a HIP
 // event pair counted as that many traces).
@@ -739,13 +744,15 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stre
       return hip_fail(ctx, pe, "probe trace launch");
     }
     p.plan_valid = 1u;
-    p.cam_lists_ready = 1u;  // the probe built them
+    if (builds_camera_lists(ran)) p.cam_lists_ready = 1u;  // the probe built them
   }
   HRT_HIP(ctx, hipEventRecord(ev.start, stream));
   hipError_t e = hrt::launch_trace(p, variant, stream, &ctx->last_kernel, &ctx->last_block);
   // the persistent kernels recorded this trace's tile costs: the lane's next trace can follow a plan
   lane.plan_valid = e == hipSuccess && persistent_kernel(ctx->last_kernel);
-  if (e == hipSuccess) {
+  // (only a kernel that built the lists leaves them valid: a LITERAL / BRUTE trace from this position
+  // followed by a bundle kernel must rebuild them)
+  if (e == hipSuccess && builds_camera_lists(ctx->last_kernel)) {
     lane.cam_ready = true;
     std::memcpy(lane.cam_key, key, sizeof key);
   }
@@ -808,8 +815,10 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
     if ((st = ensure_ring(ctx)) != HRT_OK) return st;
     if (ctx->ring) {
       slot = (int)ctx->ring_next;
-      for (const auto& pd : ctx->pend)
-        if (pd.slot == (uint32_t)slot && (st = hrt::flush_combines(ctx)) != HRT_OK) return st;
+      // (the flush clears ctx->pend: decide first, flush outside the loop)
+      const bool busy = std::any_of(ctx->pend.begin(), ctx->pend.end(),
+                                    [&](const auto& pd) { return pd.slot == (uint32_t)slot; });
+      if (busy && (st = hrt::flush_combines(ctx)) != HRT_OK) return st;
     }
   }
   int l = 0;

@@ -196,7 +196,8 @@ __device__ __forceinline__ HitRecord resolve_hit(const Scene& sc, const Closest&
 }
 
 // environment_light, raytracing.glsl:290-294
-__device__ __forceinline__ f3 environment_light(const hrt_push_constants& pc, f3 d) {
+template <class PC>
+__device__ __forceinline__ f3 environment_light(const PC& pc, f3 d) {
   if (!pc.use_environment_light) return mk(0.0f, 0.0f, 0.0f);
   const float a = 0.5f * (d.y + 1.0f);
   const float oma = 1.0f - a;
@@ -586,6 +587,8 @@ struct Diag {
   uint32_t sec_stage2 = 0, sec_front = 0;
   uint32_t bvh_trips = 0, bvh_leaf_trips = 0;  // BUNDLE_BVH: wave-level traversal trips
   uint32_t band_max = 0, band_len = 0;          // BUNDLE_WQ: longest band list per batch / every lane's, summed
+  uint32_t sky_items = 0;                       // work items run by sky_samples
+  uint64_t cyc_sky = 0;                         // ... and their shader clocks
 };
 
 __device__ __forceinline__ float wave_min_all(float v) {  // all 64 lanes active
@@ -1927,6 +1930,55 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 // at least sec_batch lanes wait or no primary segment is left in the wave, then all waiting lanes run
 // their bounce segment together.  Per-pixel order of work (and so every result) is unchanged.
 
+// Sky items.  A wave whose primary list is empty (tl.ok, tl.n == 0) in a scene without spheres tests
+// nothing in world_hit_tile, so each primary segment of its lanes is a miss: raytracing.glsl:318-346's
+// miss branch (environment light, path ends, no RNG draw after get_ray_dir) and the lane's next sample
+// starts at once.  The fused loop then spends its whole trip on bookkeeping (ballots, the bounce-batch
+// vote, the list loop's set-up, shade_step's branches) around one ray generation.  sky_samples runs the
+// lanes' num_samples such segments as a plain loop instead, two samples per trip (once each sample's
+// three hashes are drawn, their ray generations are independent), with the fused loop's per-pixel
+// arithmetic in the same order: the same colour, RNG state, segment and test counts.
+#ifndef HRT_SKY_LOOP
+#define HRT_SKY_LOOP 1
+#endif
+__device__ __forceinline__ void sky_segment(const KArgs K, const TileList& tl, bool active, f3 centre, uint32_t& state,
+                                            f3& colour, uint32_t& tests) {
+  const auto& pc = K->pc;
+  const f3 d = normalize(get_ray_dir(pc, centre, state));
+  // world_hit_tile's test count: the octant table (one lane read, all 64 lanes run this), or the
+  // literal AABB test off its domain
+  const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
+  const uint32_t oct_tests = (uint32_t)__shfl((int)tl.tsum, (int)oct, 64);
+  if (__builtin_expect(tl.aabb_ok && fabsf(d.x) <= 1.5f && fabsf(d.y) <= 1.5f && fabsf(d.z) <= 1.5f, 1)) {
+    tests += oct_tests;
+  } else if (active) {
+    const f3 o = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
+    for (int m = 0; m < pc.num_meshes; ++m)
+      if (aabb_pass(K->meshes[m], o, d)) tests += K->meshes[m].len;
+  }
+  // shade_step's miss (p.light = 0 + environment light) and the caller's colour += light * (1, 1, 1)
+  const f3 light = mk(0.0f, 0.0f, 0.0f) + environment_light(pc, d);
+  colour = colour + light * mk(1.0f, 1.0f, 1.0f);
+}
+// The lanes' whole pixels.  ALL 64 lanes run it (wave-uniform condition; the idle lanes' results are
+// dropped); tl holds the wave's octant table.
+__device__ __forceinline__ void sky_samples(const TileList& tl, bool active, f3 centre, uint32_t& state, f3& colour,
+                                            uint32_t& segs, uint32_t& tests) {
+  const KArgs K = kargs();
+  const int ns = K->pc.num_samples;
+  uint32_t t = 0;
+  int s = 0;
+  for (; s + 2 <= ns; s += 2) {
+    sky_segment(K, tl, active, centre, state, colour, t);
+    sky_segment(K, tl, active, centre, state, colour, t);
+  }
+  if (s < ns) sky_segment(K, tl, active, centre, state, colour, t);
+  if (active) {
+    segs += ns > 0 ? (uint32_t)ns : 0u;
+    tests += t;
+  }
+}
+
 // kBounceWqR: BUNDLE_WQ with node margins from each member's own R (HRT_OPT_WQ_NODE_RADIUS = 2)
 enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2, kBounceWq = 3, kBounceWqR = 4 };
 constexpr bool is_wq(int b) { return b == kBounceWq || b == kBounceWqR; }
@@ -1962,6 +2014,18 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   p.bounce = pc.max_bounces + 1;
   bool done = !active;
   Diag dg;
+  if (HRT_SKY_LOOP && tl.ok && tl.n == 0u && pc.num_spheres == 0) {  // wave-uniform: every segment a miss
+    const uint64_t s0 = (D && P.diag) ? __builtin_readcyclecounter() : 0;
+    sky_samples(tl, active, centre, state, colour, segs, tests);
+    const uint32_t ns = pc.num_samples > 0 ? (uint32_t)pc.num_samples : 0u;
+    if (co.w == 0) co.work += 2u + 3u * ns;  // the fused loop's work units for these trips
+    if (D && P.diag) {
+      dg.prim_iters += ns;
+      dg.sky_items += 1u;
+      dg.cyc_sky += __builtin_readcyclecounter() - s0;
+    }
+    done = true;
+  }
   while (__any(!done)) {
     if (!done && p.bounce > pc.max_bounces) {
       if (sample >= pc.num_samples) {
@@ -2084,6 +2148,10 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[4], (unsigned long long)dg.sec_considered);
     atomicAdd(&P.diag[5], (unsigned long long)dg.sec_survivors);
     atomicAdd(&P.diag[6], (unsigned long long)dg.sec_lanes);
+    if (dg.sky_items) {
+      atomicAdd(&P.diag[19], (unsigned long long)dg.sky_items);
+      atomicAdd(&P.diag[20], (unsigned long long)dg.cyc_sky);
+    }
   }
   if (D && P.diag && (Bounce == kBounceBvh || is_wq(Bounce))) {
     atomicAdd(&P.diag[7], (unsigned long long)dg.bvh_visits);

@@ -296,7 +296,9 @@ typedef enum hrt_diag {
   HRT_DIAG_BVH_LEAF_TRIPS = 16,    /* ... of which some lane tested a leaf */
   HRT_DIAG_BAND_SCAN_MAX = 17,     /* BUNDLE_WQ: grazing-band entries of the longest list per bounce batch, summed */
   HRT_DIAG_BAND_SCAN_LEN = 18,     /* ... of every bounce lane's list, summed */
-  HRT_NUM_DIAG = 19
+  HRT_DIAG_SKY_ITEMS = 19,         /* work items (waves) whose primary list is empty: every segment a miss */
+  HRT_DIAG_SKY_CYCLES = 20,        /* ... their shader clocks per wave, summed */
+  HRT_NUM_DIAG = 21
 } hrt_diag;
 
 /* What hrt_set_scene built for BUNDLE_BVH (hrt_get_scene_info). */

@@ -448,3 +448,32 @@ def test_camera_lists_follow_the_camera(overlap):
         want = fresh(pos, k)
         assert np.array_equal(got, want), f"frame {k}: {mismatch_report(got, want)}"
     ctx.close()
+
+
+def test_camera_lists_after_a_variant_switch():
+    """A kernel that neither builds nor reads the camera lists (LITERAL, BRUTE) leaves the lane's lists as
+    they were: BUNDLE_WQ from position B, then LITERAL from A, then BUNDLE_WQ from A on the same lane must
+    rebuild A's lists (the lane was marked as holding A's lists after the LITERAL trace, and
+    the last trace read B's), giving the image of a fresh context at A."""
+    case = SceneCase("island", (96, 64), 2, 4)
+    a = np.asarray(case.camera.position, np.float32)
+    b = a + np.float32([0.7, 0.3, -0.4])
+
+    def push(pos, k):
+        pc = case.push(k)
+        pc.cam_pos[:] = [float(pos[0]), float(pos[1]), float(pos[2]), 1.0]
+        return pc
+
+    fresh = case.context(variant=_lib.KERNEL_BUNDLE_WQ)
+    fresh.trace(push(a, 3))
+    want = fresh.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+    fresh.close()
+    ctx = case.context()
+    ctx.set_option(_lib.OPT_OVERLAP, 1)
+    for variant, pos, k in ((_lib.KERNEL_BUNDLE_WQ, b, 1), (_lib.KERNEL_LITERAL, a, 2), (_lib.KERNEL_BRUTE, a, 2),
+                            (_lib.KERNEL_BUNDLE_WQ, a, 3)):
+        ctx.set_option(_lib.OPT_KERNEL_VARIANT, variant)
+        ctx.trace(push(pos, k))
+    got = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+    ctx.close()
+    assert np.array_equal(got, want), mismatch_report(got, want)

@@ -795,3 +795,54 @@ def test_headline_properties(headline):
     n = 1920 * 1080 * 64
     assert n <= st.segments <= 9 * n             # every path: 1..max_bounces+1 segments
     assert st.tri_tests <= st.segments * 1610
+
+
+def _island_split(parts):
+    """The island preset with each mesh's triangles dealt into `parts` meshes (same material): more than
+    8 meshes, so the primary AABB quirk leaves the octant table for the literal test."""
+    cam, settings = E.preset("island")
+    out = []
+    for rm in settings.mesh_data:
+        tri = rm.mesh.indices.reshape(-1, 3)
+        for p in range(parts):
+            sub = tri[p::parts]
+            if len(sub):
+                out.append(E.RayTracingMesh(E.Mesh(rm.mesh.positions, sub.reshape(-1)), rm.material))
+    settings.mesh_data = out
+    return cam, settings
+
+
+@pytest.mark.parametrize("variant", [0, 4, 7])
+@pytest.mark.parametrize("what", ["odd_spp", "no_env", "ten_meshes", "bound_at_origin", "jitter0"])
+def test_sky_items_bit_exact(what, variant):
+    """Work items whose primary list is empty run sky_samples (every segment a miss, a plain loop of the
+    lanes' samples) instead of the fused loop: the frame and counters equal the oracle's for an odd sample
+    count (the loop's remainder), without the environment light, with more than 8 meshes and with a mesh
+    bound at the camera's coordinate (the literal AABB test for the test count instead of the octant
+    table), and with zero jitter."""
+    spp, size, off = (5 if what == "odd_spp" else 4), (160, 90), 3
+    if what == "ten_meshes":
+        cam, settings = _island_split(3)
+        case = SceneCase(None, size, spp, 8, rng_offset=off, settings=settings, camera=cam)
+    else:
+        case = SceneCase("island", size, spp, 8, rng_offset=off)
+    if what == "no_env":
+        case.settings.use_environment_lighting = False
+    if what == "jitter0":
+        case.jitter = 0.0
+    if what == "bound_at_origin":  # the camera's x on the Tree mesh's max x (a zero slab distance)
+        pos = np.asarray(case.camera.position, np.float32).copy()
+        pos[0] = case.meshes[0]["max_point"][0]
+        case.camera.position = [float(v) for v in pos]
+    ref, _, seg, tt = case.oracle()
+    ctx = case.context(variant=variant)
+    for counters in (1, 2):  # the product kernel, then its diagnostics instantiation
+        ctx.set_option(_lib.OPT_COUNTERS, counters)
+        ctx.reset_stats()
+        ctx.trace(case.push())
+        st = ctx.stats()
+        img = ctx.read(_lib.IMG_TRACE)
+        assert np.array_equal(img, ref), mismatch_report(img, ref)
+        assert (st.segments, st.tri_tests) == (seg, tt)
+    assert ctx.diagnostics()["sky_items"] > 0  # the path ran
+    ctx.close()

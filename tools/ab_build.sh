@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B builds of libhip_raytrace.so with extra compile definitions (device and host code), for HRT_LIB=... experiments:
 #   bash tools/ab_build.sh <name> -DHRT_WQ_DEEP=0u ...   -> epq_raytracer_amd/build/ab_<name>/libhip_raytrace.so
-# EXP_PATCH=1: build from a copy of the sources with tools/exp/phase_experiments.patch applied -- the
+# EXP_PATCH=<file.patch>: build from a copy of the sources with that patch applied (EXP_PATCH=1:
+# tools/exp/phase_experiments.patch) -- e.g. the
 # timing-only phase experiments (-DHRT_EXP_TWICE=<phase>: a phase run twice on opaque copies of its inputs;
 # -DHRT_EXP_ONE_NORMALIZE: wrong frames; -DHRT_IEEE_DIV: the compiler's division sequences), which the
 # product sources do not carry.  The patch is against the sources of its commit.
@@ -14,7 +15,8 @@ SRC=$ROOT/epq_raytracer_amd/csrc
 if [ -n "$EXP_PATCH" ]; then
   TMP=$OUT/src; rm -rf $TMP; mkdir -p $TMP/epq_raytracer_amd
   cp -r $SRC $TMP/epq_raytracer_amd/csrc
-  (cd $TMP && patch -s -p1 < $ROOT/tools/exp/phase_experiments.patch)
+  PATCH=$EXP_PATCH; [ "$PATCH" == "1" ] && PATCH=$ROOT/tools/exp/phase_experiments.patch
+  (cd $TMP && patch -s -p1 < $PATCH)
   SRC=$TMP/epq_raytracer_amd/csrc
 fi
 make -s -C $SRC OUT=$OUT OBJDIR=$OUT/obj ROOT=$ROOT \
