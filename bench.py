@@ -71,6 +71,9 @@ def parse():
                     help="after the timed steps: frames of the per-frame dispatch loop (compute_then_render) "
                          "reported as per_frame_dispatch_ms (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length (0 = skip)")
+    ap.add_argument("--comm-timeout-ms", type=int, default=60000,
+                    help="HRT_OPT_COMM_TIMEOUT_MS: a collective (hrt_comm_init, the gather) whose peers do not "
+                         "arrive within this fails on every rank instead of hanging")
     ap.add_argument("--pmc-json", default=None,
                     help="rocprofv3 PMC record of this build and workload (tools/pmc.sh); default "
                          "profiles/pmc_traffic.json for island, profiles/pmc_traffic_<scene>.json otherwise")
@@ -139,6 +142,35 @@ def spawn_ranks(n: int, argv, cmd=None, poll_s: float = 0.1) -> int:
     return status
 
 
+def rank_record(ctx, rank, world, lib_gather, kern_ms, gather_ms, segs) -> dict:
+    """What one rank reports to rank 0 for an N > 1 line: the communicator the LIBRARY has
+    (hrt_comm_info: did RCCL see N ranks?), its per-frame kernel time and its gather's wall time."""
+    crank, cworld, transport = ctx.comm_info() if lib_gather else (rank, world, 0)
+    return {"rank": rank, "rccl_rank": int(crank), "rccl_world": int(cworld), "transport": int(transport),
+            "kernel_ms": round(float(kern_ms), 4), "gather_ms": None if gather_ms is None else round(gather_ms, 4),
+            "segments": int(segs)}
+
+
+def assemble_ranks(recs: list, world: int) -> dict:
+    """The line's "ranks" object from every rank's rank_record (rank 0 first or not): the
+    communicator's world size as the ranks see it (min / max: 8 and 8 when RCCL joined all 8), the rank
+    ids it gave them, each rank's kernel time and gather time (max = what the step waited for)."""
+    recs = sorted(recs, key=lambda r: r["rank"])
+    worlds = [r["rccl_world"] for r in recs]
+    gms = [r["gather_ms"] for r in recs if r["gather_ms"] is not None]
+    return {"reported": len(recs), "world": world,
+            "rccl_world": {"min": min(worlds), "max": max(worlds)},
+            "rccl_ranks": [r["rccl_rank"] for r in recs],
+            "rccl_ok": len(recs) == world and min(worlds) == max(worlds) == world
+                       and sorted(r["rccl_rank"] for r in recs) == list(range(world)),
+            "transport": sorted({r["transport"] for r in recs}),
+            "kernel_ms": [r["kernel_ms"] for r in recs],
+            "kernel_ms_max": max(r["kernel_ms"] for r in recs),
+            "gather_ms": [r["gather_ms"] for r in recs],
+            "gather_ms_max": max(gms) if gms else None,
+            "segments": [r["segments"] for r in recs]}
+
+
 def main():
     args = parse()
     how, world = resolve_launch(args.gpus, os.environ)
@@ -186,9 +218,14 @@ def main():
 
     lib_gather = dist_on and not gloo
     if lib_gather:  # RCCL communicator inside the library: rank 0's id shared through torch.distributed
+        ctx.set_option(_lib.OPT_COMM_TIMEOUT_MS, args.comm_timeout_ms)
         uid = [E.HrtContext.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(uid[0], rank, world)
+        try:
+            ctx.comm_init(uid[0], rank, world)
+        except _lib.HrtError as e:  # (the library's error text; every rank fails, none waits past the timeout)
+            print(f"bench.py rank {rank}/{world}: {e}", file=sys.stderr, flush=True)
+            os._exit(3)
     local = torch.empty((ctx.local_rows, W, 4), dtype=torch.uint8, device=coll_dev) if dist_on and gloo else None
     full = torch.empty((H, W, 4), dtype=torch.uint8, device=f"cuda:{device}") if lib_gather and rank == 0 else None
 
@@ -236,6 +273,16 @@ def main():
 
     st = ctx.stats()
     segs, tests = st.segments, st.tri_tests
+    # the gather's own wall time (one more present after the timed region: the library's status
+    # all-reduce + ncclGather + row assembly, or the gloo all-gather)
+    gather_ms = None
+    if dist_on:
+        dist.barrier()
+        tg = time.perf_counter()
+        present()
+        ctx.synchronize()
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
     last_trace = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8) if world == 1 else None
     gathered = full.cpu().numpy() if (dist_on and rank == 0 and full is not None) else None
     # the realtime loop (compute_then_render per frame, src/main.rs:41-57): consecutive traces overlap
@@ -260,7 +307,11 @@ def main():
     last_frame = frame - 1 - (args.realtime_frames + 6 if rt_ms is not None else 0)
     kernel_sym = _lib.kernel_symbol(st.last_kernel, st.last_block,  # what HRT_KERNEL_AUTO resolved to
                                     node_r=_lib.wq_node_radius(ctx.scene_info()))
+    ranks = None
     if dist_on:
+        recs = [None] * world
+        dist.all_gather_object(recs, rank_record(ctx, rank, world, lib_gather, kern_ms, gather_ms, segs))
+        ranks = assemble_ranks(recs, world)
         t = torch.tensor([elapsed, kern_ms, rt_ms or 0.0], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
@@ -283,7 +334,7 @@ def main():
         algo_bytes = BYTES_PER_PIXEL_FRAME * pix_local + (len(raytrace.tris) * 64 + len(raytrace.meshes) * 80)
         # the timed launch's frames (the PMC record must be of the same launch shape)
         roof = pmc_roofline(args, world, kernel_sym, kern_ms, tests_per_frame, ctx.local_rows / H,
-                            min(args.steps, fpl) if fpl > 1 else 1)
+                            max(1, st.last_frames))  # (as the library split the steps into launches)
         line = {
             "metric": (f"Mrays/s ({args.scene}.obj {W}x{H} {args.spp}spp {args.bounces}-bounce path-trace segments "
                        "per second)"),
@@ -343,6 +394,8 @@ def main():
         if world == 1 and args.cpu_seconds > 0:
             line["cpu_baseline"], line["parity_sample"] = cpu_baseline(args, raytrace, camera, last_frame,
                                                                        last_trace)
+        if ranks is not None:
+            line["ranks"] = ranks
         if dist_on and args.verify:
             line["gather_check"] = verify_gather(args, gathered, settings, camera, device, last_frame)
         print(json.dumps(line), flush=True)

@@ -63,10 +63,11 @@ class Layout(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("segments", c_uint64), ("tri_tests", c_uint64), ("traces", c_uint64), ("accumulates", c_uint64),
                 ("last_trace_ms", c_float), ("total_trace_ms", c_float), ("wave_steps", c_uint64),
-                ("last_kernel", c_uint32), ("last_block", c_uint32)]
+                ("last_kernel", c_uint32), ("last_block", c_uint32), ("last_frames", c_uint32),
+                ("reserved", c_uint32)]
 
 
-ABI_VERSION = 3  # HRT_ABI_VERSION this binding's signatures describe
+ABI_VERSION = 4  # HRT_ABI_VERSION this binding's signatures describe
 HRT_OK = 0
 STATUS_NAMES = {0: "HRT_OK", 1: "HRT_ERR_INVALID_ARGUMENT", 2: "HRT_ERR_NO_DEVICE", 3: "HRT_ERR_OUT_OF_MEMORY",
                 4: "HRT_ERR_NO_SCENE", 5: "HRT_ERR_HIP", 6: "HRT_ERR_IO", 7: "HRT_ERR_COMM"}
@@ -122,7 +123,7 @@ EXPORTED_SYMBOLS = (
     "hrt_abi_version", "hrt_build_id", "hrt_debug_build", "hrt_debug_check_guards", "hrt_create", "hrt_destroy", "hrt_set_scene", "hrt_trace", "hrt_accumulate", "hrt_compute_n",
     "hrt_read_image", "hrt_load_accumulator", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
     "hrt_get_diagnostics", "hrt_get_tile_profile", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
-    "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory", "hrt_debug_math_check", "hrt_debug_math_check_rng", "hrt_debug_band_flatten",
+    "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory", "hrt_debug_math_check", "hrt_debug_math_check_rng", "hrt_debug_band_flatten", "hrt_debug_wq_protocol",
     "hrt_stream", "hrt_last_error", "hrt_comm_unique_id", "hrt_comm_init", "hrt_comm_init_all", "hrt_comm_info",
     "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
     "hrt_debug_bvh_build", "hrt_debug_bvh_wq_nodes",
@@ -192,6 +193,7 @@ def load(debug: bool = False) -> ctypes.CDLL:
         "hrt_debug_math_check": (c_int32, [c_int32, c_uint32, c_uint32, P]),
         "hrt_debug_math_check_rng": (c_int32, [c_int32, P]),
         "hrt_debug_band_flatten": (c_int32, [c_int32, P, P, c_uint32, P, P]),
+        "hrt_debug_wq_protocol": (c_int32, [c_int32, c_uint32, P, P, P, P, P, P, P, P, P]),
         "hrt_debug_bvh_build": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, P, c_uint64, P, c_uint64, P,
                                           c_uint64, P, c_uint64, P, c_uint64]),
         "hrt_debug_bvh_wq_nodes": (c_int64, [P, c_uint32, P, c_uint32, c_uint32, c_uint32, P, c_uint64]),

@@ -748,6 +748,7 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stre
   }
   HRT_HIP(ctx, hipEventRecord(ev.start, stream));
   hipError_t e = hrt::launch_trace(p, variant, stream, &ctx->last_kernel, &ctx->last_block);
+  if (e == hipSuccess) ctx->last_frames = ev.frames;
   // the persistent kernels recorded this trace's tile costs: the lane's next trace can follow a plan
   lane.plan_valid = e == hipSuccess && persistent_kernel(ctx->last_kernel);
   // (only a kernel that built the lists leaves them valid: a LITERAL / BRUTE trace from this position
@@ -1040,6 +1041,8 @@ extern "C" hrt_status hrt_get_stats(hrt_context* ctx, hrt_stats* out) {
   out->wave_steps = c[2];
   out->last_kernel = (uint32_t)ctx->last_kernel;
   out->last_block = (uint32_t)ctx->last_block;
+  out->last_frames = ctx->last_frames;
+  out->reserved = 0;
   out->last_trace_ms = ctx->last_ms;
   out->total_trace_ms = ctx->total_ms;
   return HRT_OK;
@@ -1182,6 +1185,45 @@ extern "C" hrt_status hrt_debug_math_check_rng(int device, uint64_t out[3]) {
 
 // Test support: the band lists' wave flattening (hrt_kernels.hip BandFlat) on 64 given lists;
 // owner_entry[(r * 64 + l) * 2 + {0, 1}] = owner lane and entry of slot r * 64 + l, r < rounds.
+extern "C" hrt_status hrt_debug_wq_protocol(int device, uint32_t rounds, const uint32_t* cnt, const uint32_t* take,
+                                            const uint32_t* tgt, const uint64_t* val, const uint64_t seed[64],
+                                            uint32_t* popped, uint64_t* seen, uint64_t slots[64], uint32_t* depth) {
+  if (!cnt || !take || !tgt || !val || !seed || !popped || !seen || !slots || !depth || rounds == 0 || rounds > 1024)
+    return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_debug_wq_protocol: bad arguments");
+  for (uint32_t i = 0; i < rounds * 64u; ++i)
+    if (cnt[i] > 4u) return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_debug_wq_protocol: cnt > 4");
+  const size_t nr = (size_t)rounds * 64;
+  // device layout: u64 [val nr][seed 64][seen nr][slots 64], then u32 [cnt nr][take rounds][tgt nr][popped nr][depth]
+  const size_t b64 = (2 * nr + 128) * 8, b32 = (3 * nr + rounds + 1) * 4;
+  char* d = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc((void**)&d, b64 + b32);
+  unsigned long long* dval = reinterpret_cast<unsigned long long*>(d);
+  unsigned long long* dseed = dval + nr;
+  unsigned long long* dseen = dseed + 64;
+  unsigned long long* dslots = dseen + nr;
+  uint32_t* dcnt = reinterpret_cast<uint32_t*>(d + b64);
+  uint32_t* dtake = dcnt + nr;
+  uint32_t* dtgt = dtake + rounds;
+  uint32_t* dpop = dtgt + nr;
+  uint32_t* ddepth = dpop + nr;
+  if (e == hipSuccess) e = hipMemset(d, 0, b64 + b32);
+  if (e == hipSuccess) e = hipMemcpy(dval, val, nr * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dseed, seed, 64 * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dcnt, cnt, nr * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dtake, take, rounds * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dtgt, tgt, nr * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hrt::launch_wq_protocol_check(rounds, dcnt, dtake, dtgt, dval, dseed, dpop, dseen, dslots, ddepth, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(popped, dpop, nr * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(seen, dseen, nr * 8, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(slots, dslots, 64 * 8, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(depth, ddepth, 4, hipMemcpyDeviceToHost);
+  if (d) (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "hrt_debug_wq_protocol");
+  return HRT_OK;
+}
+
 extern "C" hrt_status hrt_debug_band_flatten(int device, const uint32_t n[64], const uint32_t b0[64], uint32_t rounds,
                                              uint32_t* owner_entry, uint32_t* total) {
   if (!n || !b0 || !owner_entry || !total || rounds == 0 || rounds > 4096)

@@ -143,6 +143,7 @@ struct hrt_context {
   bool diag_on = false;
   uint32_t sec_batch = 0;  // HRT_OPT_SECONDARY_BATCH (0 = auto per kernel, launch_trace)
   int last_kernel = 0, last_block = 0;  // what the last hrt_trace launched (hrt_stats)
+  uint32_t last_frames = 0;             // ... and the frames that launch held
 
   struct Import {
     hipExternalMemory_t mem;

@@ -102,6 +102,11 @@ hipError_t launch_math_check(uint32_t n, uint32_t seed, unsigned long long* out,
 hipError_t launch_band_flatten_check(const uint32_t* n, const uint32_t* b0, uint32_t rounds, uint32_t* out,
                                      hipStream_t stream);  // BandFlat on 64 given lists
 hipError_t launch_math_check_rng(unsigned long long* out, hipStream_t stream);  // all 2^32 RNG states
+// the pair traversal's LDS handoff protocol on a scripted wave (hrt_debug_wq_protocol)
+hipError_t launch_wq_protocol_check(uint32_t rounds, const uint32_t* cnt, const uint32_t* take, const uint32_t* tgt,
+                                    const unsigned long long* val, const unsigned long long* seed, uint32_t* popped,
+                                    unsigned long long* seen, unsigned long long* slots, uint32_t* depth,
+                                    hipStream_t stream);
 // BUNDLE_WQ's per-wave node-stack capacity for an image of n_nodes records with groups of `width` and
 // leaves of at most max_leaf triangles (0: does not fit the LDS)
 uint32_t wq_stack_cap(uint32_t n_nodes, uint32_t width, uint32_t max_leaf);

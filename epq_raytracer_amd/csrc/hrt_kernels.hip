@@ -67,6 +67,36 @@ __device__ __forceinline__ Scene kscene() {
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 __device__ __forceinline__ f3 ray_at(f3 o, f3 d, float t) { return o + d * t; }  // :158-160
 
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+
+// Cross-lane handoffs through LDS (the pair stacks, the closest-hit slots, the band marks).  A lane's
+// store read by ANOTHER lane is a data exchange between threads, so it is written as one: relaxed
+// wavefront-scope atomics for the exchanged words and a wavefront-scope acquire-release fence between
+// every producer and its consumers (wave_handoff).  On gfx950 these compile to the plain ds_read /
+// ds_write and no instruction at all -- a wave's LDS accesses complete in program order -- but they
+// stop the compiler from reasoning per lane: with plain accesses it may forward a lane's own store to
+// its later load of the same word or move a load above another lane's store (r03: that forwarding lost
+// the band marks of lists starting at a lane with no list; tests/test_gpu_boundary.py's protocol tests
+// run these helpers through hrt_debug_wq_protocol).
+template <class T>
+__device__ __forceinline__ void lds_put(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+template <class T>
+__device__ __forceinline__ T lds_get(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+#ifndef HRT_WQ_HANDOFF
+#define HRT_WQ_HANDOFF 1
+#endif
+__device__ __forceinline__ void wave_handoff() {
+#if HRT_WQ_HANDOFF
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#endif
+}
+
 // local (compacted) row -> global row, hrt_create_info partition.
 __device__ __forceinline__ uint32_t global_row(uint32_t lr, const TraceParams& /*P*/) {
   const KArgs K = kargs();  // (once per work item)
@@ -787,7 +817,7 @@ __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool a
       const uint32_t cnt = (uint32_t)__popcll(mask);
       if (t.n + cnt > cap) return t;  // ok stays false: per-iteration cull
       if (lds) {  // lane-parallel append in buffer order
-        if (keep) lds[t.n + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = k | ((uint32_t)m << 27);
+        if (keep) lds_put(&lds[t.n + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))], k | ((uint32_t)m << 27));
         t.n += cnt;
       } else {
         while (mask) {  // few survivors: append each to the next lane
@@ -800,9 +830,7 @@ __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool a
     }
   }
   t.ok = true;
-  // the wave reads its own LDS writes back; a wave's LDS accesses complete in order, so only the
-  // compiler needs fencing
-  __builtin_amdgcn_wave_barrier();
+  wave_handoff();  // the list's entries (other lanes' stores) before the reads of world_hit_tile
   return t;
 }
 
@@ -833,10 +861,40 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
   float best_k = c.t * kOnePlus;
   const kfloat* ct = to_const(HRT_SHADE_KARGS ? kargs()->cam_tris : P.cam_tris);
   auto entry = [&](uint32_t i) {
-    return tl.lds ? __builtin_amdgcn_readfirstlane(tl.lds[i]) : (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
+    return tl.lds ? __builtin_amdgcn_readfirstlane(lds_get(&tl.lds[i])) : (uint32_t)__builtin_amdgcn_readlane((int)tl.v, (int)i);
   };
   // (r03: requesting the next entry's record before this one's test was slower, island 2.259 -> 2.338)
-  for (uint32_t i = 0; i < tl.n; ++i) {
+#ifndef HRT_LIST_UNIFORM
+#define HRT_LIST_UNIFORM 1
+#endif
+  // (the list length through readfirstlane: hipcc had lost its uniformity through build_tile_list's
+  // early returns and ran the entry loop as a divergent loop with a VGPR trip count)
+  const uint32_t n = HRT_LIST_UNIFORM ? __builtin_amdgcn_readfirstlane(tl.n) : tl.n;
+#ifndef HRT_LIST_PAIRS
+#define HRT_LIST_PAIRS 0
+#endif
+#if HRT_LIST_PAIRS
+  // entries two at a time: both records requested before either is tested (one exposed K$ round trip
+  // per pair), then tested in list order (the second sees the first's closest hit)
+  for (uint32_t i = 0; i < n; i += 2) {
+    const bool two = i + 1u < n;
+    const uint32_t e0 = entry(i), e1 = two ? entry(i + 1u) : e0;
+    const uint32_t k0 = e0 & 0x07FFFFFFu, m0 = e0 >> 27, k1 = e1 & 0x07FFFFFFu, m1 = e1 >> 27;
+    const bool p0 = prim && ((pm >> (8 * m0)) & 1ull), p1 = two && prim && ((pm >> (8 * m1)) & 1ull);
+    if (!__any(p0 | p1)) continue;
+    const kf16 R0 = ld_rec(ct, k0), R1 = ld_rec(ct, k1);
+    const float dn0 = p0 ? dot(d, mk(R0[12], R0[13], R0[14])) : 0.0f;
+    const float dn1 = p1 ? dot(d, mk(R1[12], R1[13], R1[14])) : 0.0f;
+    if (__any(dn0 < 0.0f))
+      primary_exact_rec(make_float4(R0[0], R0[1], R0[2], R0[3]), make_float4(R0[4], R0[5], R0[6], R0[7]),
+                        make_float4(R0[8], R0[9], R0[10], R0[11]), dn0, d, m0, c, best_k);
+    if (__any(dn1 < 0.0f))
+      primary_exact_rec(make_float4(R1[0], R1[1], R1[2], R1[3]), make_float4(R1[4], R1[5], R1[6], R1[7]),
+                        make_float4(R1[8], R1[9], R1[10], R1[11]), dn1, d, m1, c, best_k);
+  }
+  if (n) return;
+#endif
+  for (uint32_t i = 0; i < n; ++i) {
     const uint32_t e = entry(i);
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
     const bool pass = prim && ((pm >> (8 * m)) & 1ull);
@@ -1526,8 +1584,22 @@ __device__ __forceinline__ bool wq_tri_accept(const float4& A, const float4& B, 
   return !(dist < 0.0f) && !(u < 0.0f) && !(v < 0.0f) && !(w < 0.0f) && dist > 0.001f;
 }
 
+// closest-hit slot of ray (lane) r: seeded by its owner, lowered by any lane, read for pruning by any
+// lane (a stale value only prunes less: the slot never increases) and finally by its owner
+__device__ __forceinline__ void wq_slot_seed(unsigned long long* slot, uint32_t lane, unsigned long long v) {
+  lds_put(&slot[lane], v);
+}
+__device__ __forceinline__ void wq_slot_lower(unsigned long long* slot, uint32_t r, unsigned long long v) {
+  __hip_atomic_fetch_min(&slot[r], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
 __device__ __forceinline__ float wq_slot_t(const WqLds& wq, uint32_t r) {
-  return __uint_as_float(reinterpret_cast<const uint32_t*>(wq.slot)[2 * r + 1]);
+  return __uint_as_float(lds_get(reinterpret_cast<const uint32_t*>(wq.slot) + (2 * r + 1)));
+}
+// pair stacks: the lanes with `push` append v in lane order at the wave-uniform top n
+__device__ __forceinline__ void wq_push(uint32_t* st, uint32_t& n, bool push, uint32_t v) {
+  const unsigned long long b = __ballot(push);
+  if (push) lds_put(&st[n + lanes_below(b)], v);
+  n += (uint32_t)__popcll(b);
 }
 
 // Leaf prim k for ray r (origin o, direction d, mesh filter mask): test and lower the ray's slot.
@@ -1540,13 +1612,10 @@ __device__ __forceinline__ void wq_leaf_prim(const float4* __restrict__ pr, cons
   // first, so the four record loads issue together (one L2 round trip per triangle step, not two)
   if (wq_tri_accept(A, B, C, N, o, d, wq_slot_t(wq, r) * kOnePlus, dist) && ((mask >> m) & 1ull)) {
     const uint32_t id = ((m << 26) | __builtin_bit_cast(uint32_t, C.w)) + 1u;
-    atomicMin(&wq.slot[r], ((unsigned long long)__float_as_uint(dist) << 32) | id);
+    wq_slot_lower(wq.slot, r, ((unsigned long long)__float_as_uint(dist) << 32) | id);
   }
 }
 
-__device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-}
 
 // The grazing-band lists of a wave's lanes laid end to end (world_hit_bounce_wq): lane l's list of n
 // entries starts at global slot pos (exclusive prefix of the lengths), total slots.  slot(base, own)
@@ -1560,14 +1629,15 @@ struct BandFlat {
   uint32_t lane, n, pos, total, delta;  // delta = b0 - pos: entry of slot g = the owner's delta + g (mod 2^32)
   uint32_t carry;
   __device__ __forceinline__ uint32_t slot(uint32_t base, uint32_t& own) {
-    // (relaxed atomics: a slot's mark is another lane's store, so with plain accesses hipcc forwarded
-    // this lane's own clearing store to the load on the path where the lane marks nothing -- losing the
-    // start marks of lists that begin at the slot of a lane with no list of its own.  A wave's LDS
-    // accesses complete in program order, so no fence is needed on the hardware side.)
-    __hip_atomic_store(&marks[lane], (uint8_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    // (a slot's mark is another lane's store: with plain accesses hipcc forwarded this lane's own
+    // clearing store to the load on the path where the lane marks nothing -- losing the start marks of
+    // lists that begin at the slot of a lane with no list of its own; lds_put / lds_get / wave_handoff)
+    lds_put(&marks[lane], (uint8_t)0);
+    wave_handoff();  // every clear before any lane's mark
     const uint32_t rel = pos - base;
-    if (n && rel < 64u) __hip_atomic_store(&marks[rel], (uint8_t)(lane + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    const uint32_t v = __hip_atomic_load(&marks[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (n && rel < 64u) lds_put(&marks[rel], (uint8_t)(lane + 1u));
+    wave_handoff();  // every mark before any lane's read
+    const uint32_t v = lds_get(&marks[lane]);
     const unsigned long long m = __ballot(v != 0u) & (lane == 63u ? ~0ull : (2ull << lane) - 1ull);
     const uint32_t s = m ? 63u - (uint32_t)__builtin_clzll(m) : 0u;
     const uint32_t sv = (uint32_t)__shfl((int)v, (int)s, 64);
@@ -1619,16 +1689,19 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   uint32_t band_tests = 0, band_lmax = 0;
   // the ray's closest hit so far (spheres, the irregular list) seeds its slot
   const uint32_t id0 = c.kind == 2 ? ((c.mesh << 26) | c.idx) + 1u : 0u;
-  wq.slot[lane] = ((unsigned long long)__float_as_uint(c.t) << 32) | id0;
+  wq_slot_seed(wq.slot, lane, ((unsigned long long)__float_as_uint(c.t) << 32) | id0);
+  wave_handoff();  // seeds before any lane's read or lowering
   uint32_t tc = 0, tri_pairs = 0, steps = 0;
   // one step of 64 waiting triangle pairs (the band rounds' overflow guard)
   auto tri_step64 = [&]() {
     tc -= 64u;
-    const uint32_t e = wq.ts[tc + lane], r = e & 63u;
+    wave_handoff();
+    const uint32_t e = lds_get(&wq.ts[tc + lane]), r = e & 63u;
     const unsigned long long rm =
         ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
         (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
     wq_leaf_prim(prims, wq, e >> 6, r, rm, shfl3(o, r), shfl3(d, r));
+    wave_handoff();  // these pops before the round's pushes into their words
     tri_pairs += 64u;
     ++steps;
   };
@@ -1705,9 +1778,9 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       const unsigned long long pb = __ballot(push);
 #if HRT_WQ_PUSH_DUMP
       // (non-pushing lanes store into the node stack's last word: empty during the band rounds)
-      (push ? wq.ts[tc + lanes_below(pb)] : wq.ns[wq.ncap - 1u]) = (q << 6) | own;
+      lds_put(push ? &wq.ts[tc + lanes_below(pb)] : &wq.ns[wq.ncap - 1u], (q << 6) | own);
 #else
-      if (push) wq.ts[tc + lanes_below(pb)] = (q << 6) | own;
+      if (push) lds_put(&wq.ts[tc + lanes_below(pb)], (q << 6) | own);
 #endif
       tc += (uint32_t)__popcll(pb);
       band_tests += push ? 1u : 0u;
@@ -1725,7 +1798,8 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   }
   const uint32_t rcnt = rvis ? rinfo >> 27 : 0u;
   const unsigned long long rb = __ballot(rvis && rcnt == 0u);
-  if (rvis && rcnt == 0u) wq.ns[lanes_below(rb)] = (rinfo << 6) | lane;  // inner root: its children's group
+  wave_handoff();  // the band rounds' marks (in the node stack's words) before the root pushes
+  if (rvis && rcnt == 0u) lds_put(&wq.ns[lanes_below(rb)], (rinfo << 6) | lane);  // inner root: its children's group
   uint32_t nc = (uint32_t)__popcll(rb);
   {  // leaf root (a scene of at most leaf-size triangles): its triangles, after any band pairs
     uint32_t pre = tc, tot = 0;
@@ -1735,7 +1809,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       pre += lanes_below(bb) << b;
       tot += (uint32_t)__popcll(bb) << b;
     }
-    for (uint32_t j = 0; j < rcnt; ++j) wq.ts[pre + j] = (((rinfo & 0x07FFFFFFu) + j) << 6) | lane;
+    for (uint32_t j = 0; j < rcnt; ++j) lds_put(&wq.ts[pre + j], (((rinfo & 0x07FFFFFFu) + j) << 6) | lane);
     tc += tot;
   }
   const uint32_t width = K->bvh_wq_width;  // the image's largest group
@@ -1755,7 +1829,8 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     node_pairs += nn;
     tri_pairs += tn;
     const bool is_node = lane < nn, is_tri = lane >= nn && lane < nn + tn;
-    const uint32_t e = is_node ? wq.ns[nc + lane] : is_tri ? wq.ts[tc + lane - nn] : lane;
+    wave_handoff();  // the last step's pushes and slot lowerings before this step's pops and reads
+    const uint32_t e = is_node ? lds_get(&wq.ns[nc + lane]) : is_tri ? lds_get(&wq.ts[tc + lane - nn]) : lane;
     const uint32_t r = e & 63u;
     const f3 ro = shfl3(o, r), rd = shfl3(d, r);
     const unsigned long long rm =
@@ -1853,6 +1928,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     }
     // kept inner members: slot-major (every lane's slot 0, then slot 1, ...; the ordering may have
     // moved a member to any slot)
+    wave_handoff();  // this step's pops before the pushes that reuse their words
 #pragma unroll
     for (int k = 0; k < (int)kWqSlots; ++k) {
       const bool push = pe[k] != ~0u;
@@ -1860,9 +1936,9 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #if HRT_WQ_PUSH_DUMP
       // every lane stores (no branch): the others into the stack's last word, which no entry reaches
       // (the overflow test keeps nc + width nn below ncap)
-      wq.ns[push ? nc + lanes_below(bk) : wq.ncap - 1u] = pe[k];
+      lds_put(&wq.ns[push ? nc + lanes_below(bk) : wq.ncap - 1u], pe[k]);
 #else
-      if (push) wq.ns[nc + lanes_below(bk)] = pe[k];
+      if (push) lds_put(&wq.ns[nc + lanes_below(bk)], pe[k]);
 #endif
       nc += (uint32_t)__popcll(bk);
     }
@@ -1888,13 +1964,13 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
                      f3 = (li[3] & 0x07FFFFFFu) - s3;
       for (uint32_t j = 0; j < cnt; ++j) {
         const uint32_t f = j >= s3 ? f3 : j >= s2 ? f2 : j >= s1 ? f1 : f0;
-        wq.ts[at + j] = ((f + j) << 6) | r;
+        lds_put(&wq.ts[at + j], ((f + j) << 6) | r);
       }
 #else
 #pragma unroll
       for (int k = 0; k < (int)kWqSlots; ++k) {
         const uint32_t c = li[k] >> 27, first = li[k] & 0x07FFFFFFu;
-        for (uint32_t j = 0; j < c; ++j) wq.ts[at + j] = ((first + j) << 6) | r;
+        for (uint32_t j = 0; j < c; ++j) lds_put(&wq.ts[at + j], ((first + j) << 6) | r);
         at += c;
       }
 #endif
@@ -1907,8 +1983,9 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       }
     }
   }
+  wave_handoff();  // every lowering before the owners' reads
   if (sec) {
-    const unsigned long long s = wq.slot[lane];
+    const unsigned long long s = lds_get(&wq.slot[lane]);
     const uint32_t id = (uint32_t)s;
     if (id != 0u) c = Closest{__uint_as_float((uint32_t)(s >> 32)), 2, (id - 1u) & 0x03FFFFFFu, (id - 1u) >> 26};
   }
@@ -1986,7 +2063,7 @@ constexpr bool is_wq(int b) { return b == kBounceWq || b == kBounceWqR; }
 template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, const CullSrc& csrc,
                                                   const BvhSrc& bsrc, uint32_t* list_lds, Coop& co,
-                                                  uint32_t frame = 0) {
+                                                  uint32_t frame = 0, uint32_t nrun = 1) {
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes, P.tri_nhat};
   const hrt_push_constants& pc = P.pc;
   const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
@@ -2014,20 +2091,37 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   p.bounce = pc.max_bounces + 1;
   bool done = !active;
   Diag dg;
+  // Frame runs (tile_loop): the item's frames frame .. frame + nrun - 1 of a multi-frame launch, one
+  // after the other per lane -- a lane that finishes its pixel in one frame starts the pixel's next
+  // frame (rng_offset + f, its own image) at once instead of idling until the wave's slowest lane ends.
+  uint32_t fr = 0;
   if (HRT_SKY_LOOP && tl.ok && tl.n == 0u && pc.num_spheres == 0) {  // wave-uniform: every segment a miss
     const uint64_t s0 = (D && P.diag) ? __builtin_readcyclecounter() : 0;
-    sky_samples(tl, active, centre, state, colour, segs, tests);
+    for (;; ++fr) {
+      sky_samples(tl, active, centre, state, colour, segs, tests);
+      if (fr + 1u >= nrun) break;
+      if (active) store_pixel(P, x, lr, div3(colour, (float)pc.num_samples), frame + fr);
+      colour = mk(0.0f, 0.0f, 0.0f);
+      state = (pc.rng_offset + frame + fr + 1u) * 719393u + id;
+    }
     const uint32_t ns = pc.num_samples > 0 ? (uint32_t)pc.num_samples : 0u;
-    if (co.w == 0) co.work += 2u + 3u * ns;  // the fused loop's work units for these trips
+    if (co.w == 0) co.work += (2u + 3u * ns) * nrun;  // the fused loop's work units for these trips
     if (D && P.diag) {
-      dg.prim_iters += ns;
-      dg.sky_items += 1u;
+      dg.prim_iters += ns * nrun;
+      dg.sky_items += nrun;
       dg.cyc_sky += __builtin_readcyclecounter() - s0;
     }
     done = true;
   }
   while (__any(!done)) {
     if (!done && p.bounce > pc.max_bounces) {
+      if (sample >= pc.num_samples && fr + 1u < nrun) {  // the pixel's next frame of the run
+        store_pixel(P, x, lr, div3(colour, (float)pc.num_samples), frame + fr);
+        ++fr;
+        colour = mk(0.0f, 0.0f, 0.0f);
+        sample = 0;
+        state = (pc.rng_offset + frame + fr) * 719393u + id;
+      }
       if (sample >= pc.num_samples) {
         done = true;
       } else {
@@ -2104,7 +2198,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   if (co.w != 0) return;  // cooperative tile: wave 0 of the group writes the results
   if (active) {
     colour = div3(colour, (float)pc.num_samples);
-    store_pixel(P, x, lr, colour, frame);
+    store_pixel(P, x, lr, colour, frame + fr);
   }
   if (co.defer) {
     unsigned long long s, t;
@@ -2261,7 +2355,7 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
       const uint32_t tile = __builtin_amdgcn_readfirstlane(P.items[hi]) & kItemTileMask;
       const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
       co.work = 0;
-      body(tx * 8 + (lane & 7), ty * 8 + (lane >> 3), co, hf);
+      body(tx * 8 + (lane & 7), ty * 8 + (lane >> 3), co, hf, 1u);
       prev_cost = __builtin_amdgcn_readfirstlane(co.work);
       prev_tile = tile;
     }
@@ -2282,6 +2376,9 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
   // The threshold sum of the planner (sched[6]) is summed per wave and added once.
 #ifndef HRT_GRAB
 #define HRT_GRAB 4u
+#endif
+#ifndef HRT_FRAME_RUN
+#define HRT_FRAME_RUN 1
 #endif
   constexpr uint32_t kGrab = HRT_GRAB;
   const uint32_t resident = gridDim.x * (BLOCK / 64);
@@ -2304,9 +2401,12 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
       cur = __builtin_amdgcn_readfirstlane(t);
       end = cur + g;
     }
-    t = cur++;
+    t = cur;
     if (t >= n) break;
     const uint32_t ti = t / nf, tf = t - ti * nf;
+    // the grabbed indices of this item's next frames run as one body (frame runs, trace_fused_split)
+    const uint32_t run = HRT_FRAME_RUN ? min(min(end, n) - t, nf - tf) : 1u;
+    cur += run;
     const uint32_t* items = K->items;
     const uint32_t item = items ? __builtin_amdgcn_readfirstlane(items[ti]) : 0u;
     const uint32_t tile = items ? item & kItemTileMask : ti, lk = (item >> 22) & 7u, sub = (item >> 25) & 63u;
@@ -2318,7 +2418,7 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     const uint64_t t0 = __builtin_readcyclecounter();
     if (hot) __builtin_amdgcn_s_setprio(3);
     solo.work = 0;
-    body(x, lr, solo, tf);
+    body(x, lr, solo, tf, run);
     if (hot) __builtin_amdgcn_s_setprio(0);
     // cost: the work count where the body keeps one (BUNDLE_CULL_LDS), else shader clocks / 16
     const uint64_t c = CoopOk ? (uint64_t)solo.work : (__builtin_readcyclecounter() - t0) >> 4;
@@ -2419,8 +2519,8 @@ __global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
   unsigned long long* ex = reinterpret_cast<unsigned long long*>(lds_tris + 3 * P.n_tris);
   for (uint32_t k = threadIdx.x; k < 3 * 64; k += BLOCK) ex[k] = ~0ull;
   __syncthreads();
-  tile_loop<BLOCK, true>(P, ex, &s_item, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f) {
-    trace_fused_split<kBounceCull, D>(P, x, lr, CullLds{lds_tris}, BvhGlobal{}, nullptr, co, f);
+  tile_loop<BLOCK, true>(P, ex, &s_item, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f, uint32_t nr) {
+    trace_fused_split<kBounceCull, D>(P, x, lr, CullLds{lds_tris}, BvhGlobal{}, nullptr, co, f, nr);
   });
 }
 
@@ -2439,8 +2539,8 @@ __global__ __launch_bounds__(BLOCK) void trace_bundle_cull_lds(TraceParams P) {
                    reinterpret_cast<uint32_t*>(base + 512) + P.wq_ncap, P.wq_ncap};                            \
     __syncthreads();                                                                                            \
     const float4* T = reinterpret_cast<const float4*>(P.tris);                                                  \
-    tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f) {           \
-      trace_fused_split<BOUNCE, D>(P, x, lr, CullGlobal{T, to_const(T)}, wq, nullptr, co, f);                   \
+    tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f, uint32_t nr) { \
+      trace_fused_split<BOUNCE, D>(P, x, lr, CullGlobal{T, to_const(T)}, wq, nullptr, co, f, nr);               \
     });                                                                                                         \
   }
 template <bool D>
@@ -2464,9 +2564,9 @@ __global__ __launch_bounds__(1024) void trace_bundle_bvh_lds(TraceParams P) {
   for (uint32_t k = threadIdx.x; k < nm; k += 1024) kbase[k] = P.bvh_keybase[k];
   __syncthreads();
   const float4* T = reinterpret_cast<const float4*>(P.tris);
-  tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f) {
+  tile_loop<1024, false>(P, nullptr, nullptr, [&](uint32_t x, uint32_t lr, Coop& co, uint32_t f, uint32_t nr) {
     trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhLds{nodes, lds_tris, entries, kbase},
-                                     nullptr, co, f);
+                                     nullptr, co, f, nr);
   });
 }
 
@@ -2705,6 +2805,43 @@ __global__ __launch_bounds__(64) void band_flatten_check(const uint32_t* n_in, c
     out[(r * 64u + lane) * 2u + 1u] = k;
   }
   if (lane == 0) out[rounds * 128u] = total;
+}
+
+// hrt_debug_wq_protocol: the pair traversal's LDS handoffs on a scripted run of one wave -- per round,
+// the top take[r] entries popped (lane l < take reads entry n - take + l), each lane's slot read and
+// lowering of slot tgt (tgt >= 64: none), then the lanes' pushes (lane l pushes cnt[r][l] <= 4 entries
+// (r << 16 | l << 8 | k), slot-major as the node steps push) -- in the product kernel's order, with
+// its helpers (wq_push, lds_get, wq_slot_*, wave_handoff).
+constexpr uint32_t kProtoCap = 8192;
+__global__ __launch_bounds__(64) void wq_protocol_check(uint32_t rounds, const uint32_t* cnt, const uint32_t* take,
+                                                        const uint32_t* tgt, const unsigned long long* val,
+                                                        const unsigned long long* seed, uint32_t* popped,
+                                                        unsigned long long* seen, unsigned long long* slots_out,
+                                                        uint32_t* depth_out) {
+  __shared__ unsigned long long slot[64];
+  __shared__ uint32_t st[kProtoCap];
+  const uint32_t lane = threadIdx.x & 63u;
+  wq_slot_seed(slot, lane, seed[lane]);
+  wave_handoff();
+  uint32_t n = 0;
+  for (uint32_t r = 0; r < rounds; ++r) {
+    const uint32_t tk = min(take[r], n);
+    n -= tk;
+    wave_handoff();
+    popped[r * 64u + lane] = lane < tk ? lds_get(&st[n + lane]) : ~0u;
+    const uint32_t t = tgt[r * 64u + lane];
+    if (t < 64u) {
+      seen[r * 64u + lane] = lds_get(&slot[t]);
+      wq_slot_lower(slot, t, val[r * 64u + lane]);
+    }
+    const uint32_t c = cnt[r * 64u + lane];
+    wave_handoff();
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; ++k) wq_push(st, n, c > k && n + 256u <= kProtoCap, (r << 16) | (lane << 8) | k);
+  }
+  wave_handoff();
+  slots_out[lane] = lds_get(&slot[lane]);
+  if (lane == 0) *depth_out = n;
 }
 
 __global__ __launch_bounds__(256) void math_check(uint32_t n, uint32_t seed, unsigned long long* out) {
@@ -3024,6 +3161,13 @@ hipError_t launch_assemble_rows(const uint32_t* gathered, uint32_t* frame, uint3
   return hipGetLastError();
 }
 
+hipError_t launch_wq_protocol_check(uint32_t rounds, const uint32_t* cnt, const uint32_t* take, const uint32_t* tgt,
+                                    const unsigned long long* val, const unsigned long long* seed, uint32_t* popped,
+                                    unsigned long long* seen, unsigned long long* slots, uint32_t* depth,
+                                    hipStream_t stream) {
+  wq_protocol_check<<<1, 64, 0, stream>>>(rounds, cnt, take, tgt, val, seed, popped, seen, slots, depth);
+  return hipGetLastError();
+}
 hipError_t launch_band_flatten_check(const uint32_t* n, const uint32_t* b0, uint32_t rounds, uint32_t* out,
                                      hipStream_t stream) {
   band_flatten_check<<<1, 64, 0, stream>>>(n, b0, rounds, out);

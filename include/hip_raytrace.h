@@ -39,10 +39,11 @@
 extern "C" {
 #endif
 
-/* 3 (r03): hrt_debug_band_flatten.
+/* 4 (r04): hrt_debug_wq_protocol; HRT_DIAG_SKY_ITEMS / HRT_DIAG_SKY_CYCLES (HRT_NUM_DIAG 21).
+ * 3 (r03): hrt_debug_band_flatten.
  * 2 (r03): HRT_ERR_COMM, HRT_IMG_LOCAL, HRT_OPT_COMM_TIMEOUT_MS, collective error agreement;
  * hrt_debug_bvh_wq_nodes' width parameter; HRT_NUM_DIAG / HRT_NUM_SCENE_INFO grown (r02). */
-#define HRT_ABI_VERSION 3u
+#define HRT_ABI_VERSION 4u
 
 typedef enum hrt_status {
   HRT_OK = 0,
@@ -161,6 +162,9 @@ typedef struct hrt_stats {
                              efficiency = segments / (64 * wave_steps) */
   uint32_t last_kernel;   /* hrt_kernel the last trace ran (HRT_KERNEL_AUTO resolved) */
   uint32_t last_block;    /* its workgroup size (threads) */
+  uint32_t last_frames;   /* frames the last trace launch held (hrt_compute_n packs up to
+                             HRT_OPT_FRAMES_PER_LAUNCH into one launch; 1 for hrt_trace) (ABI 4) */
+  uint32_t reserved;
 } hrt_stats;
 
 typedef struct hrt_context hrt_context;
@@ -446,6 +450,16 @@ hrt_status hrt_debug_math_check_rng(int device, uint64_t out[3]);
  * *total = the slots in all (the sum of n). */
 hrt_status hrt_debug_band_flatten(int device, const uint32_t n[64], const uint32_t b0[64], uint32_t rounds,
                                   uint32_t* owner_entry, uint32_t* total);
+/* Test support: the pair traversal's cross-lane LDS handoffs (BUNDLE_WQ's stacks and closest-hit slots) on
+ * a scripted run of one wave of 64 lanes over `rounds` <= 1024 rounds.  Slot l starts at seed[l].  Round r:
+ * the top min(take[r], depth) stack entries are popped (popped[r * 64 + l] = the entry lane l < take
+ * read, else 0xFFFFFFFF); lane l with tgt[r * 64 + l] < 64 reads that slot (seen[r * 64 + l]) and lowers it
+ * to val[r * 64 + l] (u64 minimum); then lane l pushes cnt[r * 64 + l] <= 4 entries (r << 16 | l << 8 | k),
+ * k-major over the lanes in lane order (while the stack holds at most 8192 - 256).  slots[l] = the final
+ * slots, *depth = the final stack depth. */
+hrt_status hrt_debug_wq_protocol(int device, uint32_t rounds, const uint32_t* cnt, const uint32_t* take,
+                                 const uint32_t* tgt, const uint64_t* val, const uint64_t seed[64], uint32_t* popped,
+                                 uint64_t* seen, uint64_t slots[64], uint32_t* depth);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
 /* The context's HIP stream (hipStream_t), for callers that interoperate: work enqueued on it after

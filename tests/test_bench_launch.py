@@ -68,3 +68,39 @@ def test_bench_refuses_more_rccl_ranks_than_gpus():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "needs 2 GPUs" in r.stderr
     assert "metric" not in r.stdout
+
+
+def test_assemble_ranks_says_whether_rccl_saw_every_rank():
+    """The N > 1 line's "ranks" object: the communicator's world as each rank's
+    library reports it (hrt_comm_info), the rank ids, and each rank's kernel and gather times."""
+    def rec(r, cw=8, cr=None, g=1.5):
+        return {"rank": r, "rccl_rank": r if cr is None else cr, "rccl_world": cw, "transport": 1,
+                "kernel_ms": 0.3 + 0.01 * r, "gather_ms": None if g is None else g + r, "segments": 1000 + r}
+    ok = bench.assemble_ranks([rec(r) for r in reversed(range(8))], 8)
+    assert ok["rccl_ok"] and ok["rccl_world"] == {"min": 8, "max": 8} and ok["rccl_ranks"] == list(range(8))
+    assert ok["kernel_ms"][0] == 0.3 and ok["kernel_ms_max"] == 0.37 and ok["gather_ms_max"] == 8.5
+    assert ok["segments"] == [1000 + r for r in range(8)] and ok["transport"] == [1]
+    split = bench.assemble_ranks([rec(r, cw=1, cr=0) if r == 3 else rec(r) for r in range(8)], 8)
+    assert not split["rccl_ok"] and split["rccl_world"] == {"min": 1, "max": 8}
+    assert not bench.assemble_ranks([rec(r) for r in range(7)], 8)["rccl_ok"]  # a rank never reported
+    assert bench.assemble_ranks([rec(r, cw=2, g=None) for r in range(2)], 2)["gather_ms_max"] is None
+
+
+def test_rank_records_reach_rank_0_over_gloo(tmp_path):
+    """Two stand-in ranks (gloo on the CPU, the real rank_record / all_gather_object / assemble_ranks with a
+    stand-in context whose comm_info is the library's answer) produce rank 0's "ranks" object."""
+    out = tmp_path / "ranks.json"
+    code = (
+        "import json, os, sys; sys.path.insert(0, sys.argv[2]); import bench, torch.distributed as dist\n"
+        "dist.init_process_group('gloo'); r, w = dist.get_rank(), dist.get_world_size()\n"
+        "class Ctx:\n"
+        "    def comm_info(self): return (r, w, 1)\n"
+        "recs = [None] * w\n"
+        "dist.all_gather_object(recs, bench.rank_record(Ctx(), r, w, True, 0.5 + r, 2.0 * (r + 1), 10 + r))\n"
+        "if r == 0: open(sys.argv[1], 'w').write(json.dumps(bench.assemble_ranks(recs, w)))\n"
+        "dist.barrier(); dist.destroy_process_group()\n")
+    assert bench.spawn_ranks(2, [str(out), ROOT], cmd=[sys.executable, "-c", code]) == 0
+    import json
+    got = json.loads(out.read_text())
+    assert got["rccl_ok"] and got["rccl_world"] == {"min": 2, "max": 2} and got["rccl_ranks"] == [0, 1]
+    assert got["kernel_ms"] == [0.5, 1.5] and got["gather_ms"] == [2.0, 4.0] and got["gather_ms_max"] == 4.0

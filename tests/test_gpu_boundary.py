@@ -477,3 +477,72 @@ def test_camera_lists_after_a_variant_switch():
     got = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
     ctx.close()
     assert np.array_equal(got, want), mismatch_report(got, want)
+
+
+def _wq_protocol_model(cnt, take, tgt, val, seed):
+    """Host model of hrt_debug_wq_protocol: a LIFO stack and u64 minimum slots, round by round."""
+    rounds = len(take)
+    stack, slots = [], [int(v) for v in seed]
+    popped = np.full((rounds, 64), 0xFFFFFFFF, np.uint64)
+    lo = np.zeros((rounds, 64), np.uint64)   # seen[r][l] must be <= the slot before round r's lowerings
+    hi = np.zeros((rounds, 64), np.uint64)   # ... and >= the slot after them
+    for r in range(rounds):
+        tk = min(int(take[r]), len(stack))
+        top = stack[len(stack) - tk:]
+        del stack[len(stack) - tk:]
+        popped[r, :tk] = top
+        before = list(slots)
+        for lane in range(64):
+            t = int(tgt[r, lane])
+            if t < 64:
+                slots[t] = min(slots[t], int(val[r, lane]))
+        for lane in range(64):
+            t = int(tgt[r, lane])
+            if t < 64:
+                lo[r, lane], hi[r, lane] = slots[t], before[t]
+        for k in range(4):
+            room = len(stack) + 256 <= 8192  # wave-uniform, before the k-th pushes
+            for lane in range(64):
+                if cnt[r, lane] > k and room:
+                    stack.append((r << 16) | (lane << 8) | k)
+    return popped, lo, hi, np.array(slots, np.uint64), len(stack)
+
+
+@pytest.mark.parametrize("case", ["balanced", "deep", "drain", "sparse_slots", "random"])
+def test_wq_handoff_protocol_matches_host(case):
+    """The pair traversal's cross-lane LDS handoffs (wq_push and the pops of the node / triangle stacks, the
+    closest-hit slots' seed / read / lowering / final read, each ordered by wave_handoff) on scripted
+    rounds of one wave: every popped entry, every slot read and the final slots equal a host model of a
+    LIFO stack and u64 minimum slots (one such handoff produced wrong frames)."""
+    seed_ = 100 + ["balanced", "deep", "drain", "sparse_slots", "random"].index(case)
+    rng = np.random.default_rng(seed_)
+    rounds = 96
+    cnt = rng.integers(0, 5, (rounds, 64)).astype(np.uint32)
+    take = rng.integers(0, 65, rounds).astype(np.uint32)
+    if case == "deep":
+        take[:] = rng.integers(0, 40, rounds)
+    elif case == "drain":
+        cnt[rounds // 2:] = 0
+        take[rounds // 2:] = 64
+    elif case == "random":
+        cnt[rng.random((rounds, 64)) < 0.5] = 0
+    tgt = rng.integers(0, 64, (rounds, 64)).astype(np.uint32)
+    tgt[rng.random((rounds, 64)) < (0.8 if case == "sparse_slots" else 0.3)] = 64  # no slot access
+    val = rng.integers(0, 1 << 62, (rounds, 64), dtype=np.uint64)
+    seed = rng.integers(1 << 61, 1 << 63, 64, dtype=np.uint64)
+    popped = np.zeros((rounds, 64), np.uint32)
+    seen = np.zeros((rounds, 64), np.uint64)
+    slots = np.zeros(64, np.uint64)
+    depth = np.zeros(1, np.uint32)
+    lib = _lib.load()
+    _lib.check(lib.hrt_debug_wq_protocol(0, rounds, _lib.ptr(cnt), _lib.ptr(take), _lib.ptr(tgt), _lib.ptr(val),
+                                         _lib.ptr(seed), _lib.ptr(popped), _lib.ptr(seen), _lib.ptr(slots),
+                                         _lib.ptr(depth)), "hrt_debug_wq_protocol")
+    want_pop, lo, hi, want_slots, want_depth = _wq_protocol_model(cnt, take, tgt, val, seed)
+    assert int(depth[0]) == want_depth
+    bad = np.argwhere(popped.astype(np.uint64) != want_pop)
+    assert bad.size == 0, f"{len(bad)} popped entries differ, first (round, lane) {bad[:3].tolist()}"
+    m = tgt < 64
+    assert (seen[m] <= hi[m]).all(), "a slot read missed an earlier round's lowering"
+    assert (seen[m] >= lo[m]).all(), "a slot read below the slot's value after its round"
+    assert np.array_equal(slots, want_slots)
