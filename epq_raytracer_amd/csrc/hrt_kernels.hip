@@ -127,6 +127,56 @@ __device__ __forceinline__ f3 get_ray_dir(const PC& pc, f3 c, uint32_t& state) {
                   __builtin_fmaf(M[10], nc.z, __builtin_fmaf(M[6], nc.y, M[2] * nc.x)));
   return normalize(w);
 }
+#ifndef HRT_NORM_UNIFORM
+#define HRT_NORM_UNIFORM 0
+#endif
+#ifndef HRT_SKY_ZERO
+#define HRT_SKY_ZERO 0
+#endif
+// get_ray_dir for the sky loop (all 64 lanes run it).  Zero: the caller has checked, for the whole
+// item, that jitter_size is finite and every active lane's centre has finite c.x != 0 and c.y != 0.  Then the
+// zero components of t1 = ((0, 0, 1) cr j) s2 and t2 = ((0, 1, 0) sr j) s3 are signed zeros (cr, sr,
+// s2, s3 are finite, s2, s3 >= +0), c.x + t1.x + t2.x == c.x and c.y + t1.y == c.y exactly, and only
+// t2.z's sign can matter (when c.z + t1.z is a zero): sign(sr) ^ sign(j).  The same bits as
+// get_ray_dir with 8 fewer VALU.
+template <bool Zero, class PC>
+__device__ __forceinline__ f3 get_ray_dir_sky(const PC& pc, f3 c, uint32_t& state) {
+  if constexpr (!Zero) {
+#if HRT_NORM_UNIFORM
+    const float r = (u01(hash(state)) * 2.0f) * 3.14159265358979323846f;
+    float sr, cr;
+    spec_sincos_angle(r, sr, cr);
+    const float j = pc.jitter_size;
+    const float s2 = sqrt_rng(u01(hash(state)));
+    const f3 t1 = ((mk(0.0f, 0.0f, 1.0f) * cr) * j) * s2;
+    const float s3 = sqrt_rng(u01(hash(state)));
+    const f3 t2 = ((mk(0.0f, 1.0f, 0.0f) * sr) * j) * s3;
+    const f3 nc = (c + t1) + t2;
+    const auto& M = pc.cam_alignment_mat;
+    return normalize_wu(mk(__builtin_fmaf(M[8], nc.z, __builtin_fmaf(M[4], nc.y, M[0] * nc.x)),
+                           __builtin_fmaf(M[9], nc.z, __builtin_fmaf(M[5], nc.y, M[1] * nc.x)),
+                           __builtin_fmaf(M[10], nc.z, __builtin_fmaf(M[6], nc.y, M[2] * nc.x))));
+#else
+    return get_ray_dir(pc, c, state);
+#endif
+  } else {
+    const float r = (u01(hash(state)) * 2.0f) * 3.14159265358979323846f;
+    float sr, cr;
+    spec_sincos_angle(r, sr, cr);
+    const float j = pc.jitter_size;
+    const float s2 = sqrt_rng(u01(hash(state)));
+    const float t1z = (cr * j) * s2;  // ((1 cr) j) s2
+    const float s3 = sqrt_rng(u01(hash(state)));
+    const float t2y = (sr * j) * s3;
+    const float z2 = bitsf((fbits(sr) ^ fbits(j)) & 0x80000000u);  // t2.z = ((0 sr) j) s3
+    const f3 nc = mk(c.x, c.y + t2y, (c.z + t1z) + z2);
+    const auto& M = pc.cam_alignment_mat;
+    const f3 w = mk(__builtin_fmaf(M[8], nc.z, __builtin_fmaf(M[4], nc.y, M[0] * nc.x)),
+                    __builtin_fmaf(M[9], nc.z, __builtin_fmaf(M[5], nc.y, M[1] * nc.x)),
+                    __builtin_fmaf(M[10], nc.z, __builtin_fmaf(M[6], nc.y, M[2] * nc.x)));
+    return HRT_NORM_UNIFORM ? normalize_wu(w) : normalize(w);
+  }
+}
 
 // intersecting_aabb, raytracing.glsl:192-210, restated with its min/max quirks (:202, :206); inv =
 // (1/d.x, 1/d.y, 1/d.z) correctly rounded (computed once per ray for all meshes).
@@ -2018,10 +2068,12 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #ifndef HRT_SKY_LOOP
 #define HRT_SKY_LOOP 1
 #endif
+template <bool Zero>
 __device__ __forceinline__ void sky_segment(const KArgs K, const TileList& tl, bool active, f3 centre, uint32_t& state,
                                             f3& colour, uint32_t& tests) {
   const auto& pc = K->pc;
-  const f3 d = normalize(get_ray_dir(pc, centre, state));
+  const f3 dir = get_ray_dir_sky<Zero>(pc, centre, state);
+  const f3 d = HRT_NORM_UNIFORM ? normalize_wu(dir) : normalize(dir);
   // world_hit_tile's test count: the octant table (one lane read, all 64 lanes run this), or the
   // literal AABB test off its domain
   const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
@@ -2045,11 +2097,21 @@ __device__ __forceinline__ void sky_samples(const TileList& tl, bool active, f3 
   const int ns = K->pc.num_samples;
   uint32_t t = 0;
   int s = 0;
-  for (; s + 2 <= ns; s += 2) {
-    sky_segment(K, tl, active, centre, state, colour, t);
-    sky_segment(K, tl, active, centre, state, colour, t);
+  if (HRT_SKY_ZERO && fabsf(K->pc.jitter_size) < __builtin_inff() &&
+      __all(!active || (centre.x != 0.0f && centre.y != 0.0f && fabsf(centre.x) < __builtin_inff() &&
+                        fabsf(centre.y) < __builtin_inff()))) {  // get_ray_dir_sky<true>'s premises
+    for (; s + 2 <= ns; s += 2) {
+      sky_segment<true>(K, tl, active, centre, state, colour, t);
+      sky_segment<true>(K, tl, active, centre, state, colour, t);
+    }
+    if (s < ns) sky_segment<true>(K, tl, active, centre, state, colour, t);
+  } else {
+    for (; s + 2 <= ns; s += 2) {
+      sky_segment<false>(K, tl, active, centre, state, colour, t);
+      sky_segment<false>(K, tl, active, centre, state, colour, t);
+    }
+    if (s < ns) sky_segment<false>(K, tl, active, centre, state, colour, t);
   }
-  if (s < ns) sky_segment(K, tl, active, centre, state, colour, t);
   if (active) {
     segs += ns > 0 ? (uint32_t)ns : 0u;
     tests += t;

@@ -100,6 +100,21 @@ __device__ __forceinline__ f3 normalize(f3 a) {
   }
   return a / __builtin_sqrtf(d2);
 }
+// normalize with the fast path chosen per WAVE: when every active lane is in the fast range (the usual
+// case for ray directions) the wave runs it without the per-lane exec-mask split around the IEEE
+// fallback (which every lane then skips); otherwise every active lane runs the IEEE spelling, which
+// is exact everywhere.  Same bits as normalize either way.
+__device__ __forceinline__ f3 normalize_wu(f3 a) {
+  const float d2 = dot(a, a);
+  const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+  const bool fast = d2 >= 0x1p-80f && d2 <= 0x1p78f && m >= 0x1p-80f;
+  if (__builtin_expect(__all(fast), 1)) {
+    const float l = sqrt_core(d2);
+    const float y = rcp_core(l);
+    return {div_core(a.x, l, y), div_core(a.y, l, y), div_core(a.z, l, y)};
+  }
+  return a / __builtin_sqrtf(d2);
+}
 // The reference's spelling of both (for the self-check).
 __device__ __forceinline__ f3 normalize_ieee(f3 a) { return a / __builtin_sqrtf(dot(a, a)); }
 // S6: GLSL 4.60 definitions.
