@@ -82,6 +82,7 @@ OPT_FRAMES_PER_LAUNCH, OPT_OVERLAP, OPT_BUSY_SPLIT, OPT_BVH_WIDTH, OPT_WQ_NODE_R
 OPT_COMM_TIMEOUT_MS, OPT_DEFER_COMBINE = 17, 18
 DEBUG_OPT_FAIL_ALLOC = 1001  # libhip_raytrace_debug.so only
 DEBUG_OPT_WQ_TRI_CAP = 1002  # libhip_raytrace_debug.so only
+DEBUG_OPT_GRAB_RUNS = 1003  # libhip_raytrace_debug.so only
 COMM_ID_BYTES = 128
 COMM_NONE, COMM_RCCL, COMM_RCCL_GROUP, COMM_DEVICE_COPY = 0, 1, 2, 3
 # hrt_kernel (include/hip_raytrace.h)
@@ -114,7 +115,8 @@ KERNEL_NAMES = {0: "auto", 1: "literal", 2: "brute", 3: "brute_lds", 4: "bundle"
 DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounce_iters", "bounce_considered",
               "bounce_survivors", "bounce_lanes", "bvh_visits", "bvh_prim_tests", "bvh_band_tests", "primary_cycles", "bounce_cycles",
               "shade_cycles", "bounce_stage2", "bounce_front", "bvh_trips",
-              "bvh_leaf_trips", "band_scan_max", "band_scan_len", "sky_items", "sky_cycles")
+              "bvh_leaf_trips", "band_scan_max", "band_scan_len", "sky_items", "sky_cycles",
+              "primary_lanes", "loop_iters", "live_lanes")
 SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh_built", "bvh_band_entries",
                     "bvh_sah_milli", "bvh_margin_milli")
 

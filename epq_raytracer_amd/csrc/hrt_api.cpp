@@ -655,6 +655,7 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.coop = ctx->coop;
   p.wq_ncap = ctx->wq_node_cap;  // request; launch_trace sizes the stacks
   p.wq_tcap = ctx->debug_wq_tri_cap;  // (debug) request
+  p.grab_always = ctx->debug_grab_runs;  // (debug) frame runs at any size
   p.plan_valid = lane.plan_valid ? 1u : 0u;
   p.num_cus = ctx->grid_cus ? std::min(ctx->grid_cus, ctx->num_cus) : ctx->num_cus;
   const bool built = s.bvh_info[HRT_SCENE_BVH_BUILT] != 0;
@@ -1395,10 +1396,15 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
         return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "wq tri cap must be 0 (auto) or in [128, 2^20]");
       ctx->debug_wq_tri_cap = (uint32_t)value;
       return HRT_OK;
+    case HRT_DEBUG_OPT_GRAB_RUNS:
+      if (value < 0 || value > 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "grab runs must be 0 or 1");
+      ctx->debug_grab_runs = (uint32_t)value;
+      return HRT_OK;
 #else
     case HRT_OPT_GRID_CUS:
     case HRT_DEBUG_OPT_FAIL_ALLOC:
     case HRT_DEBUG_OPT_WQ_TRI_CAP:
+    case HRT_DEBUG_OPT_GRAB_RUNS:
       return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "debug option: only libhip_raytrace_debug.so accepts it");
 #endif
     default:

@@ -76,6 +76,7 @@ struct TraceParams {
   uint32_t bvh_node_r;  // BUNDLE_WQ: trace_bundle_wq_nr, box margins with a per-node R (HRT_OPT_WQ_NODE_RADIUS)
   float bvh_band_tau;   // the grazing band's width tau_g the hierarchy and band lists were built for
   float bvh_band_a1;    // max over prims of |a|_1: the band's plane filter tolerance (bvh_band_nhat .w = n^.a)
+  uint32_t grab_always; // (debug, HRT_DEBUG_OPT_GRAB_RUNS) persistent waves take kGrab items per atomic to the end
 };
 
 // Per device, once: the dynamic-LDS limits of the persistent kernels (hipFuncSetAttribute).

@@ -669,6 +669,7 @@ struct Diag {
   uint32_t band_max = 0, band_len = 0;          // BUNDLE_WQ: longest band list per batch / every lane's, summed
   uint32_t sky_items = 0;                       // work items run by sky_samples
   uint64_t cyc_sky = 0;                         // ... and their shader clocks
+  uint32_t prim_lanes = 0, loop_iters = 0, live_lanes = 0;  // fused-loop lane use
 };
 
 __device__ __forceinline__ float wave_min_all(float v) {  // all 64 lanes active
@@ -2213,6 +2214,9 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
       dg.prim_iters += any_prim ? 1u : 0u;
       dg.sec_iters += run_sec ? 1u : 0u;
       dg.sec_lanes += run_sec ? nwait : 0u;
+      dg.prim_lanes += (uint32_t)__popcll(__ballot(prim));
+      dg.loop_iters += 1u;
+      dg.live_lanes += (uint32_t)__popcll(__ballot(!done));
       t0 = __builtin_readcyclecounter();
     }
     if (co.w == 0) co.work += 2u + (any_prim ? 1u + (tl.ok ? tl.n : 64u) : 0u);  // shading, primary list
@@ -2308,6 +2312,9 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
       atomicAdd(&P.diag[19], (unsigned long long)dg.sky_items);
       atomicAdd(&P.diag[20], (unsigned long long)dg.cyc_sky);
     }
+    atomicAdd(&P.diag[21], (unsigned long long)dg.prim_lanes);
+    atomicAdd(&P.diag[22], (unsigned long long)dg.loop_iters);
+    atomicAdd(&P.diag[23], (unsigned long long)dg.live_lanes);
   }
   if (D && P.diag && (Bounce == kBounceBvh || is_wq(Bounce))) {
     atomicAdd(&P.diag[7], (unsigned long long)dg.bvh_visits);
@@ -2448,7 +2455,7 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
   unsigned long long cost_sum = 0;
   for (;;) {
     const bool refill = cur >= end;  // wave-uniform
-    const uint32_t g = (uint64_t)cur + 16ull * kGrab * resident < n ? kGrab : 1u;
+    const uint32_t g = (kargs()->grab_always || (uint64_t)cur + 16ull * kGrab * resident < n) ? kGrab : 1u;
     uint32_t t = 0;
     const KArgs K = kargs();  // (per work item: not held across the item's fused loop)
     if (lane == 0) {

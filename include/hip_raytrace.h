@@ -39,7 +39,8 @@
 extern "C" {
 #endif
 
-/* 4 (r04): hrt_debug_wq_protocol; HRT_DIAG_SKY_ITEMS / HRT_DIAG_SKY_CYCLES (HRT_NUM_DIAG 21).
+/* 4 (r04): hrt_debug_wq_protocol; hrt_stats.last_frames; HRT_DIAG_SKY_* / PRIMARY_LANES / LOOP_ITERS /
+ * LIVE_LANES (HRT_NUM_DIAG 24).
  * 3 (r03): hrt_debug_band_flatten.
  * 2 (r03): HRT_ERR_COMM, HRT_IMG_LOCAL, HRT_OPT_COMM_TIMEOUT_MS, collective error agreement;
  * hrt_debug_bvh_wq_nodes' width parameter; HRT_NUM_DIAG / HRT_NUM_SCENE_INFO grown (r02). */
@@ -276,7 +277,12 @@ typedef enum hrt_option {
   /* libhip_raytrace_debug.so only (tests): BUNDLE_WQ's per-wave triangle-pair stack holds at most this
    * many pairs (0 = what fits; else >= 128, rounded down to a multiple of 64): bursts of kept leaves
    * beyond it are tested in place, the path the tests force with 128.  Results do not depend on it. */
-  HRT_DEBUG_OPT_WQ_TRI_CAP = 1002
+  HRT_DEBUG_OPT_WQ_TRI_CAP = 1002,
+  /* libhip_raytrace_debug.so only (tests): 1 = the persistent kernels' waves always take their work
+   * items 4 at a time, so a multi-frame launch runs frame runs (an item's consecutive frames in one
+   * pass, hrt_kernels.hip trace_fused_split) at any image size -- the full frames take them only while
+   * many items remain.  Results do not depend on it. */
+  HRT_DEBUG_OPT_GRAB_RUNS = 1003
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */
@@ -302,7 +308,10 @@ typedef enum hrt_diag {
   HRT_DIAG_BAND_SCAN_LEN = 18,     /* ... of every bounce lane's list, summed */
   HRT_DIAG_SKY_ITEMS = 19,         /* work items (waves) whose primary list is empty: every segment a miss */
   HRT_DIAG_SKY_CYCLES = 20,        /* ... their shader clocks per wave, summed */
-  HRT_NUM_DIAG = 21
+  HRT_DIAG_PRIMARY_LANES = 21,     /* fused loop: primary lanes of the iterations that ran the primary path */
+  HRT_DIAG_LOOP_ITERS = 22,        /* fused-loop iterations (waves) */
+  HRT_DIAG_LIVE_LANES = 23,        /* ... and their lanes not yet done, summed */
+  HRT_NUM_DIAG = 24
 } hrt_diag;
 
 /* What hrt_set_scene built for BUNDLE_BVH (hrt_get_scene_info). */

@@ -325,7 +325,7 @@ def test_production_library_rejects_debug_options():
     ctx = case.context()
     assert ctx.lib.hrt_debug_build() == 0
     for key, value in ((_lib.OPT_PRIORITY, 2), (_lib.OPT_GRID_CUS, 4), (_lib.DEBUG_OPT_FAIL_ALLOC, 1),
-                       (_lib.DEBUG_OPT_WQ_TRI_CAP, 128)):
+                       (_lib.DEBUG_OPT_WQ_TRI_CAP, 128), (_lib.DEBUG_OPT_GRAB_RUNS, 1)):
         with pytest.raises(_lib.HrtError, match="INVALID"):
             ctx.set_option(key, value)
     ctx.set_option(_lib.OPT_PRIORITY, 0)

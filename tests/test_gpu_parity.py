@@ -846,3 +846,31 @@ def test_sky_items_bit_exact(what, variant):
         assert (st.segments, st.tri_tests) == (seg, tt)
     assert ctx.diagnostics()["sky_items"] > 0  # the path ran
     ctx.close()
+
+
+@pytest.mark.parametrize("scene,variant", [("island", 9), ("cave", 9), ("island", 7), ("island", 8), ("box", 7)])
+def test_frame_runs_match_frame_loop(scene, variant):
+    """Frame runs (a persistent wave's grabbed items that are one tile's consecutive frames run as one
+    pass: each lane starts its pixel's next frame as soon as it finishes one) give the per-frame loop's
+    accumulator, last trace image and counters.  The debug library's HRT_DEBUG_OPT_GRAB_RUNS makes the
+    waves take 4 items per grab at this size (the product does so while many items remain)."""
+    case = SceneCase(scene, (75, 41), 3, 8)
+    first, n = 5, 11
+    loop = case.context(variant=variant)
+    for k in range(first, first + n):
+        loop.trace(case.push(k))
+        loop.accumulate(k)
+    a = loop.stats()
+    want_acc, want_trace = loop.read(_lib.IMG_ACCUM), loop.read(_lib.IMG_TRACE)
+    loop.close()
+    for grab in (1, 0):
+        ctx = case.context(variant=variant, debug=True,
+                           options={_lib.OPT_FRAMES_PER_LAUNCH: 16, _lib.DEBUG_OPT_GRAB_RUNS: grab})
+        ctx.compute_n(case.push(first), n)
+        b = ctx.stats()
+        got_acc, got_trace = ctx.read(_lib.IMG_ACCUM), ctx.read(_lib.IMG_TRACE)
+        ctx.close()
+        assert b.last_frames == n
+        assert np.array_equal(got_trace, want_trace), f"grab {grab}: " + mismatch_report(got_trace, want_trace)
+        assert np.array_equal(got_acc, want_acc), f"grab {grab}: " + mismatch_report(got_acc, want_acc)
+        assert (b.segments, b.tri_tests) == (a.segments, a.tri_tests)

@@ -99,6 +99,11 @@ def main():
                 d["bvh_leaf_trips_per_iter"] = d["bvh_leaf_trips"] / max(d["bounce_iters"], 1)
                 d["primary_cycles_per_iter"] = d["primary_cycles"] / max(d["primary_iters"], 1)
                 d["primary_list_len"] = d["primary_considered"] / max(d["primary_iters"], 1)
+                # fused loop (non-sky items): lanes doing primary work per primary iteration, live lanes
+                # per iteration, bounce lanes per batch -- each of 64
+                sky_iters = d.get("sky_items", 0) * case.settings.num_samples
+                d["primary_lane_use"] = d.get("primary_lanes", 0) / max(64 * (d["primary_iters"] - sky_iters), 1)
+                d["live_lane_use"] = d.get("live_lanes", 0) / max(64 * d.get("loop_iters", 0), 1)
                 d["band_max_per_batch"] = d.get("band_scan_max", 0) / max(d["bounce_iters"], 1)
                 d["band_len_per_lane"] = d.get("band_scan_len", 0) / max(d["bounce_lanes"], 1)
                 print(json.dumps(d), flush=True)

@@ -23,7 +23,7 @@ fi
 if [ -n "$DIAG" ]; then
   timeout -k 10 300 python3 tools/kbench.py --variants 0 --rounds 1 --no-ref --diag > $OUT/diag_island.jsonl 2>&1 || { echo "diag failed"; tail -5 $OUT/diag_island.jsonl; exit 1; }
   timeout -k 10 300 python3 tools/kbench.py --variants 0 --rounds 1 --no-ref --diag --scene cave > $OUT/diag_cave.jsonl 2>&1 || { echo "diag cave failed"; tail -5 $OUT/diag_cave.jsonl; exit 1; }
-  grep -h primary_iters $OUT/diag_island.jsonl $OUT/diag_cave.jsonl | python3 -c "import sys,json; [print({k: d[k] for k in ('primary_iters','sky_items','sky_cycles','primary_cycles','bounce_cycles','shade_cycles')}) for d in map(json.loads, sys.stdin)]"
+  grep -h primary_iters $OUT/diag_island.jsonl $OUT/diag_cave.jsonl | python3 -c "import sys,json; [print({k: d.get(k) for k in ('primary_iters','sky_items','sky_cycles','primary_cycles','bounce_cycles','shade_cycles','primary_lane_use','live_lane_use','loop_iters','bounce_lanes_per_iter')}) for d in map(json.loads, sys.stdin)]"
 fi
 if [ -n "$BENCH" ]; then
   timeout -k 10 600 python3 bench.py --cpu-seconds 5 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }

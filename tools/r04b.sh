@@ -4,7 +4,7 @@
 # tools/exp/r04_sky_split_timing.patch).
 set -o pipefail
 OUT=gpurun_out/r04b; mkdir -p $OUT
-bash tools/r04.sh r04b || exit 1
+DIAG=1 bash tools/r04.sh r04b || exit 1
 B=epq_raytracer_amd/build
 L=epq_raytracer_amd/lib/libhip_raytrace.so
 HRT_LIB=$B/ab_skyzn/libhip_raytrace.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -k "sky or frame_bit_exact or split_schedule" -q -x --timeout 200 --timeout-method thread > $OUT/skyzn_parity.log 2>&1 || { echo "skyzn parity failed"; tail -30 $OUT/skyzn_parity.log; exit 1; }
