@@ -945,15 +945,26 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
   }
   if (n) return;
 #endif
+#ifndef HRT_LIST_EARLY
+#define HRT_LIST_EARLY 0
+#endif
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t e = entry(i);
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
     const bool pass = prim && ((pm >> (8 * m)) & 1ull);
+#if HRT_LIST_EARLY
+    // (A/B) no early-out on the mesh vote: the record's load is issued at once and the vote runs during
+    // it (a lane without pass has dn = 0, so the entry is skipped by the dn vote below)
+    const kf16 R = ld_rec(ct, kk);
+#else
     if (!__any(pass)) continue;
+#endif
     {
     // the whole record in one load: the exact test's operands arrive with the normal (one K$ round
     // trip per entry instead of two dependent ones)
+#if !HRT_LIST_EARLY
     const kf16 R = ld_rec(ct, kk);
+#endif
     const float dn = pass ? dot(d, mk(R[12], R[13], R[14])) : 0.0f;
     if (__any(dn < 0.0f))
       primary_exact_rec(make_float4(R[0], R[1], R[2], R[3]), make_float4(R[4], R[5], R[6], R[7]),
@@ -2202,10 +2213,23 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
 #endif
       }
     }
-    const bool prim = !done && p.bounce == 0;
+    const bool ready = !done && p.bounce == 0;  // a primary segment to run
     const bool waiting = !done && p.bounce != 0;
     const uint32_t nwait = (uint32_t)__popcll(__ballot(waiting));
+#ifndef HRT_PRIM_BATCH
+#define HRT_PRIM_BATCH 0
+#endif
+#if HRT_PRIM_BATCH
+    // (A/B) primary segments wait too while a bounce batch runs and fewer than HRT_PRIM_BATCH lanes
+    // have one: the list loop's cost is per wave, not per lane.  Every iteration still runs one phase.
+    const uint32_t nready = (uint32_t)__popcll(__ballot(ready));
+    const bool run_prim = nready > 0 && (nready >= HRT_PRIM_BATCH || nwait < sec_thresh);
+    const bool prim = ready && run_prim;
+    const bool any_prim = run_prim;
+#else
+    const bool prim = ready;
     const bool any_prim = __any(prim);
+#endif
     const bool run_sec = nwait > 0 && (nwait >= sec_thresh || !any_prim);
     const bool sec = waiting && run_sec;
     Closest c{kFltMax, 0, 0u, 0u};
@@ -2441,7 +2465,7 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
   solo.defer = true;
   uint32_t prev_tile = 0xFFFFFFFFu, prev_cost = 0, prev_lk = 0;
   // Items are taken kGrab at a time while far from the end (one same-address atomic per kGrab items;
-  // the plan's longest-first order is kept, and the last 16 x kGrab items per resident wave go singly).
+  // the plan's longest-first order is kept, and the last HRT_GRAB_TAIL items per resident wave go singly).
   // The threshold sum of the planner (sched[6]) is summed per wave and added once.
 #ifndef HRT_GRAB
 #define HRT_GRAB 4u
@@ -2450,12 +2474,15 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
 #define HRT_FRAME_RUN 1
 #endif
   constexpr uint32_t kGrab = HRT_GRAB;
+#ifndef HRT_GRAB_TAIL
+#define HRT_GRAB_TAIL 64u  // items per resident wave taken singly at the end (16 x the r01s grab of 4)
+#endif
   const uint32_t resident = gridDim.x * (BLOCK / 64);
   uint32_t cur = first, end = first;
   unsigned long long cost_sum = 0;
   for (;;) {
     const bool refill = cur >= end;  // wave-uniform
-    const uint32_t g = (kargs()->grab_always || (uint64_t)cur + 16ull * kGrab * resident < n) ? kGrab : 1u;
+    const uint32_t g = (kargs()->grab_always || (uint64_t)cur + (uint64_t)HRT_GRAB_TAIL * resident < n) ? kGrab : 1u;
     uint32_t t = 0;
     const KArgs K = kargs();  // (per work item: not held across the item's fused loop)
     if (lane == 0) {
