@@ -1665,9 +1665,15 @@ __device__ __forceinline__ void wq_push(uint32_t* st, uint32_t& n, bool push, ui
 }
 
 // Leaf prim k for ray r (origin o, direction d, mesh filter mask): test and lower the ray's slot.
-__device__ __forceinline__ void wq_leaf_prim(const float4* __restrict__ pr, const WqLds& wq, uint32_t k, uint32_t r,
-                                             unsigned long long mask, f3 o, f3 d) {
-  const float4 A = pr[4 * k], B = pr[4 * k + 1], C = pr[4 * k + 2], N = pr[4 * k + 3];
+struct WqTriRec {
+  float4 A, B, C, N;
+};
+__device__ __forceinline__ WqTriRec wq_tri_rec(const float4* __restrict__ pr, uint32_t k) {
+  return WqTriRec{pr[4 * k], pr[4 * k + 1], pr[4 * k + 2], pr[4 * k + 3]};
+}
+__device__ __forceinline__ void wq_tri_test(const WqTriRec& t, const WqLds& wq, uint32_t r, unsigned long long mask,
+                                            f3 o, f3 d) {
+  const float4 &A = t.A, &B = t.B, &C = t.C, &N = t.N;
   const uint32_t m = __builtin_bit_cast(uint32_t, B.w);
   float dist;
   // the mesh filter (its quirky AABB test for this ray) joins the acceptance instead of leaving
@@ -1676,6 +1682,10 @@ __device__ __forceinline__ void wq_leaf_prim(const float4* __restrict__ pr, cons
     const uint32_t id = ((m << 26) | __builtin_bit_cast(uint32_t, C.w)) + 1u;
     wq_slot_lower(wq.slot, r, ((unsigned long long)__float_as_uint(dist) << 32) | id);
   }
+}
+__device__ __forceinline__ void wq_leaf_prim(const float4* __restrict__ pr, const WqLds& wq, uint32_t k, uint32_t r,
+                                             unsigned long long mask, f3 o, f3 d) {
+  wq_tri_test(wq_tri_rec(pr, k), wq, r, mask, o, d);
 }
 
 
@@ -1876,8 +1886,46 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   }
   const uint32_t width = K->bvh_wq_width;  // the image's largest group
   uint32_t node_pairs = 0;
+#ifndef HRT_WQ_DUAL
+#define HRT_WQ_DUAL 0
+#endif
+#ifndef HRT_WQ_DUAL_MIN
+#define HRT_WQ_DUAL_MIN 32u
+#endif
   while (nc | tc) {
     ++steps;
+#if HRT_WQ_DUAL
+    // (A/B) dual steps: up to 64 node pairs in lanes [0, nn) AND, once HRT_WQ_DUAL_MIN triangle pairs
+    // wait (or no node pair is left), up to 64 triangle pairs in lanes [0, tn).  The triangle pairs'
+    // records (global memory) are requested first and tested after the node pairs (LDS), so one step
+    // waits for both round trips at once instead of a step each.  Pruning reads a slot that a later
+    // lowering of the same step may undercut: it only keeps more, as any stale slot value does.
+    const uint32_t nn = min(64u, nc);
+    const uint32_t tn = (tc >= HRT_WQ_DUAL_MIN || nn == 0u) ? min(64u, tc) : 0u;
+    tc -= tn;
+    nc -= nn;
+    node_pairs += nn;
+    tri_pairs += tn;
+    const bool is_node = lane < nn, is_tri = lane < tn;
+    wave_handoff();  // the last step's pushes and slot lowerings before this step's pops and reads
+    const uint32_t et = is_tri ? lds_get(&wq.ts[tc + lane]) : lane;
+    const uint32_t e = is_node ? lds_get(&wq.ns[nc + lane]) : lane;
+    WqTriRec trec;
+    if (is_tri) trec = wq_tri_rec(prims, et >> 6);
+    // the triangle pairs' rays are shuffled when they are tested (LDS latency; not held across the node part)
+    auto tri_part = [&]() {
+      const uint32_t rt = et & 63u;
+      const f3 tro = shfl3(o, rt), trd = shfl3(d, rt);
+      const unsigned long long trm =
+          ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)rt, 64) << 32) |
+          (uint32_t)__shfl((int)(uint32_t)mask, (int)rt, 64);
+      if (is_tri) wq_tri_test(trec, wq, rt, trm, tro, trd);
+    };
+    if (nn == 0u) {
+      tri_part();
+      continue;
+    }
+#else
     // Step composition (wave-uniform): triangle pairs when >= 64 wait or no node pair is left; when
     // both stacks are short, one mixed step takes them all (lanes [0, nn) node pairs, then triangles).
     // (Measured, r02: filling a short node step's idle lanes with triangle pairs, or running triangle
@@ -1893,13 +1941,16 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const bool is_node = lane < nn, is_tri = lane >= nn && lane < nn + tn;
     wave_handoff();  // the last step's pushes and slot lowerings before this step's pops and reads
     const uint32_t e = is_node ? lds_get(&wq.ns[nc + lane]) : is_tri ? lds_get(&wq.ts[tc + lane - nn]) : lane;
+#endif
     const uint32_t r = e & 63u;
     const f3 ro = shfl3(o, r), rd = shfl3(d, r);
     const unsigned long long rm =
         ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
         (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
+#if !HRT_WQ_DUAL
     if (is_tri) wq_leaf_prim(prims, wq, e >> 6, r, rm, ro, rd);
     if (nn == 0u) continue;
+#endif
     // node pairs (ray r, group fc .. fc + cnt - 1): test every member.  Slot k: member k's push entry
     // (its info word << 6 | r when a kept inner node, else ~0u), sort key (minus its box entry
     // distance when pushed, else -inf), and its triangle count when a kept leaf.
@@ -2044,6 +2095,9 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         for (uint32_t j = 0; j < c; ++j) wq_leaf_prim(prims, wq, first + j, r, rm, ro, rd);
       }
     }
+#if HRT_WQ_DUAL
+    tri_part();
+#endif
   }
   wave_handoff();  // every lowering before the owners' reads
   if (sec) {
