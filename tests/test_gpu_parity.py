@@ -864,13 +864,15 @@ def test_frame_runs_match_frame_loop(scene, variant):
     want_acc, want_trace = loop.read(_lib.IMG_ACCUM), loop.read(_lib.IMG_TRACE)
     loop.close()
     for grab in (1, 0):
+        # (BUNDLE_BVH_LDS holds island's hierarchy in LDS with leaves of 4, not the auto 2)
         ctx = case.context(variant=variant, debug=True,
-                           options={_lib.OPT_FRAMES_PER_LAUNCH: 16, _lib.DEBUG_OPT_GRAB_RUNS: grab})
+                           options={_lib.OPT_FRAMES_PER_LAUNCH: 16, _lib.DEBUG_OPT_GRAB_RUNS: grab,
+                                    _lib.OPT_BVH_LEAF_SIZE: 4 if variant == 8 else 0})
         ctx.compute_n(case.push(first), n)
         b = ctx.stats()
         got_acc, got_trace = ctx.read(_lib.IMG_ACCUM), ctx.read(_lib.IMG_TRACE)
         ctx.close()
-        assert b.last_frames == n
+        assert b.last_frames == n and b.last_kernel == variant  # one persistent launch of all n frames
         assert np.array_equal(got_trace, want_trace), f"grab {grab}: " + mismatch_report(got_trace, want_trace)
         assert np.array_equal(got_acc, want_acc), f"grab {grab}: " + mismatch_report(got_acc, want_acc)
         assert (b.segments, b.tri_tests) == (a.segments, a.tri_tests)
