@@ -128,10 +128,10 @@ __device__ __forceinline__ f3 get_ray_dir(const PC& pc, f3 c, uint32_t& state) {
   return normalize(w);
 }
 #ifndef HRT_NORM_UNIFORM
-#define HRT_NORM_UNIFORM 0
+#define HRT_NORM_UNIFORM 1  // (r04b: with HRT_SKY_ZERO island 1.903 -> 1.876 ms per frame)
 #endif
 #ifndef HRT_SKY_ZERO
-#define HRT_SKY_ZERO 0
+#define HRT_SKY_ZERO 1
 #endif
 // get_ray_dir for the sky loop (all 64 lanes run it).  Zero: the caller has checked, for the whole
 // item, that jitter_size is finite and every active lane's centre has finite c.x != 0 and c.y != 0.  Then the
@@ -2554,13 +2554,19 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     t = cur;
     if (t >= n) break;
     const uint32_t ti = t / nf, tf = t - ti * nf;
-    // the grabbed indices of this item's next frames run as one body (frame runs, trace_fused_split)
-    const uint32_t run = HRT_FRAME_RUN ? min(min(end, n) - t, nf - tf) : 1u;
-    cur += run;
     const uint32_t* items = K->items;
     const uint32_t item = items ? __builtin_amdgcn_readfirstlane(items[ti]) : 0u;
     const uint32_t tile = items ? item & kItemTileMask : ti, lk = (item >> 22) & 7u, sub = (item >> 25) & 63u;
     const bool hot = item >> 31;  // heavy last time: issue priority over the light tiles' waves
+    // The grabbed indices of a light item's next frames run as one body (frame runs, trace_fused_split).
+    // A heavy item (split, or marked hot) takes its frames one at a time: its pixel chains are the
+    // launch's longest, and a run of them in one wave would outlast the launch (runs of 8 frames for
+    // every item: island 1.903 -> 2.208 ms per frame, profiles/r04/r04b_ab_island.jsonl).
+#ifndef HRT_RUN_HEAVY
+#define HRT_RUN_HEAVY 0
+#endif
+    const uint32_t run = (HRT_FRAME_RUN && (HRT_RUN_HEAVY || (!hot && lk == 0u))) ? min(min(end, n) - t, nf - tf) : 1u;
+    cur += run;
     const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
     const uint32_t j = (sub << (6u - lk)) + lane;  // the tile pixel (row-major) of this lane
     uint32_t x = tx * 8 + (j & 7u), lr = ty * 8 + (j >> 3);
