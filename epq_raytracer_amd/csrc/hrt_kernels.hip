@@ -2533,10 +2533,17 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
 #endif
   const uint32_t resident = gridDim.x * (BLOCK / 64);
   uint32_t cur = first, end = first;
+#ifndef HRT_GRAB_HEAVY
+#define HRT_GRAB_HEAVY 0  // 1: heavy items grabbed kGrab at a time like the others (r03)
+#endif
+  const uint32_t heavy_end = (HRT_GRAB_HEAVY || !P.items) ? 0u : P.sched[4] * nf;
   unsigned long long cost_sum = 0;
   for (;;) {
     const bool refill = cur >= end;  // wave-uniform
-    const uint32_t g = (kargs()->grab_always || (uint64_t)cur + (uint64_t)HRT_GRAB_TAIL * resident < n) ? kGrab : 1u;
+    // (singly, too, while in the plan's heavy prefix: grabbed together, a heavy item's frames queue behind
+    // each other on one wave -- HRT_GRAB_HEAVY)
+    const uint32_t g = (kargs()->grab_always ||
+                        ((uint64_t)cur + (uint64_t)HRT_GRAB_TAIL * resident < n && cur >= heavy_end)) ? kGrab : 1u;
     uint32_t t = 0;
     const KArgs K = kargs();  // (per work item: not held across the item's fused loop)
     if (lane == 0) {
@@ -2632,6 +2639,7 @@ __global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves,
   }
   sched[1] = prio > 1 ? heavy_items : pos;  // prio 2: heavy items only (diagnostics)
   sched[2] = heavy;
+  sched[4] = heavy_items;  // the plan's first heavy_items items are the heavy tiles' (tile_loop grabs them singly)
   sched[3] = hb;
 }
 // Item word: tile | log2(items of the tile) << 22 | item index s << 25 | heavy << 31 (tile_loop).
