@@ -921,50 +921,15 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
   // (the list length through readfirstlane: hipcc had lost its uniformity through build_tile_list's
   // early returns and ran the entry loop as a divergent loop with a VGPR trip count)
   const uint32_t n = HRT_LIST_UNIFORM ? __builtin_amdgcn_readfirstlane(tl.n) : tl.n;
-#ifndef HRT_LIST_PAIRS
-#define HRT_LIST_PAIRS 0
-#endif
-#if HRT_LIST_PAIRS
-  // entries two at a time: both records requested before either is tested (one exposed K$ round trip
-  // per pair), then tested in list order (the second sees the first's closest hit)
-  for (uint32_t i = 0; i < n; i += 2) {
-    const bool two = i + 1u < n;
-    const uint32_t e0 = entry(i), e1 = two ? entry(i + 1u) : e0;
-    const uint32_t k0 = e0 & 0x07FFFFFFu, m0 = e0 >> 27, k1 = e1 & 0x07FFFFFFu, m1 = e1 >> 27;
-    const bool p0 = prim && ((pm >> (8 * m0)) & 1ull), p1 = two && prim && ((pm >> (8 * m1)) & 1ull);
-    if (!__any(p0 | p1)) continue;
-    const kf16 R0 = ld_rec(ct, k0), R1 = ld_rec(ct, k1);
-    const float dn0 = p0 ? dot(d, mk(R0[12], R0[13], R0[14])) : 0.0f;
-    const float dn1 = p1 ? dot(d, mk(R1[12], R1[13], R1[14])) : 0.0f;
-    if (__any(dn0 < 0.0f))
-      primary_exact_rec(make_float4(R0[0], R0[1], R0[2], R0[3]), make_float4(R0[4], R0[5], R0[6], R0[7]),
-                        make_float4(R0[8], R0[9], R0[10], R0[11]), dn0, d, m0, c, best_k);
-    if (__any(dn1 < 0.0f))
-      primary_exact_rec(make_float4(R1[0], R1[1], R1[2], R1[3]), make_float4(R1[4], R1[5], R1[6], R1[7]),
-                        make_float4(R1[8], R1[9], R1[10], R1[11]), dn1, d, m1, c, best_k);
-  }
-  if (n) return;
-#endif
-#ifndef HRT_LIST_EARLY
-#define HRT_LIST_EARLY 0
-#endif
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t e = entry(i);
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
     const bool pass = prim && ((pm >> (8 * m)) & 1ull);
-#if HRT_LIST_EARLY
-    // (A/B) no early-out on the mesh vote: the record's load is issued at once and the vote runs during
-    // it (a lane without pass has dn = 0, so the entry is skipped by the dn vote below)
-    const kf16 R = ld_rec(ct, kk);
-#else
     if (!__any(pass)) continue;
-#endif
     {
     // the whole record in one load: the exact test's operands arrive with the normal (one K$ round
     // trip per entry instead of two dependent ones)
-#if !HRT_LIST_EARLY
     const kf16 R = ld_rec(ct, kk);
-#endif
     const float dn = pass ? dot(d, mk(R[12], R[13], R[14])) : 0.0f;
     if (__any(dn < 0.0f))
       primary_exact_rec(make_float4(R[0], R[1], R[2], R[3]), make_float4(R[4], R[5], R[6], R[7]),
@@ -1886,46 +1851,8 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   }
   const uint32_t width = K->bvh_wq_width;  // the image's largest group
   uint32_t node_pairs = 0;
-#ifndef HRT_WQ_DUAL
-#define HRT_WQ_DUAL 0
-#endif
-#ifndef HRT_WQ_DUAL_MIN
-#define HRT_WQ_DUAL_MIN 32u
-#endif
   while (nc | tc) {
     ++steps;
-#if HRT_WQ_DUAL
-    // (A/B) dual steps: up to 64 node pairs in lanes [0, nn) AND, once HRT_WQ_DUAL_MIN triangle pairs
-    // wait (or no node pair is left), up to 64 triangle pairs in lanes [0, tn).  The triangle pairs'
-    // records (global memory) are requested first and tested after the node pairs (LDS), so one step
-    // waits for both round trips at once instead of a step each.  Pruning reads a slot that a later
-    // lowering of the same step may undercut: it only keeps more, as any stale slot value does.
-    const uint32_t nn = min(64u, nc);
-    const uint32_t tn = (tc >= HRT_WQ_DUAL_MIN || nn == 0u) ? min(64u, tc) : 0u;
-    tc -= tn;
-    nc -= nn;
-    node_pairs += nn;
-    tri_pairs += tn;
-    const bool is_node = lane < nn, is_tri = lane < tn;
-    wave_handoff();  // the last step's pushes and slot lowerings before this step's pops and reads
-    const uint32_t et = is_tri ? lds_get(&wq.ts[tc + lane]) : lane;
-    const uint32_t e = is_node ? lds_get(&wq.ns[nc + lane]) : lane;
-    WqTriRec trec;
-    if (is_tri) trec = wq_tri_rec(prims, et >> 6);
-    // the triangle pairs' rays are shuffled when they are tested (LDS latency; not held across the node part)
-    auto tri_part = [&]() {
-      const uint32_t rt = et & 63u;
-      const f3 tro = shfl3(o, rt), trd = shfl3(d, rt);
-      const unsigned long long trm =
-          ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)rt, 64) << 32) |
-          (uint32_t)__shfl((int)(uint32_t)mask, (int)rt, 64);
-      if (is_tri) wq_tri_test(trec, wq, rt, trm, tro, trd);
-    };
-    if (nn == 0u) {
-      tri_part();
-      continue;
-    }
-#else
     // Step composition (wave-uniform): triangle pairs when >= 64 wait or no node pair is left; when
     // both stacks are short, one mixed step takes them all (lanes [0, nn) node pairs, then triangles).
     // (Measured, r02: filling a short node step's idle lanes with triangle pairs, or running triangle
@@ -1941,16 +1868,13 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const bool is_node = lane < nn, is_tri = lane >= nn && lane < nn + tn;
     wave_handoff();  // the last step's pushes and slot lowerings before this step's pops and reads
     const uint32_t e = is_node ? lds_get(&wq.ns[nc + lane]) : is_tri ? lds_get(&wq.ts[tc + lane - nn]) : lane;
-#endif
     const uint32_t r = e & 63u;
     const f3 ro = shfl3(o, r), rd = shfl3(d, r);
     const unsigned long long rm =
         ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
         (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
-#if !HRT_WQ_DUAL
     if (is_tri) wq_leaf_prim(prims, wq, e >> 6, r, rm, ro, rd);
     if (nn == 0u) continue;
-#endif
     // node pairs (ray r, group fc .. fc + cnt - 1): test every member.  Slot k: member k's push entry
     // (its info word << 6 | r when a kept inner node, else ~0u), sort key (minus its box entry
     // distance when pushed, else -inf), and its triangle count when a kept leaf.
@@ -2095,9 +2019,6 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         for (uint32_t j = 0; j < c; ++j) wq_leaf_prim(prims, wq, first + j, r, rm, ro, rd);
       }
     }
-#if HRT_WQ_DUAL
-    tri_part();
-#endif
   }
   wave_handoff();  // every lowering before the owners' reads
   if (sec) {

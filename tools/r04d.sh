@@ -11,3 +11,13 @@ AB_BATCH=20 timeout -k 10 1000 bash tools/ab.sh 3 $L $B/ab_gh/libhip_raytrace.so
 python3 tools/ab_summary.py $OUT/ab_island.jsonl
 AB_BATCH=20 timeout -k 10 600 bash tools/ab.sh 2 $L $B/ab_gh/libhip_raytrace.so $B/ab_g8/libhip_raytrace.so $B/ab_pb8/libhip_raytrace.so -- --scene cave > $OUT/ab_cave.jsonl 2>&1 || { echo "ab cave failed"; tail -5 $OUT/ab_cave.jsonl; exit 1; }
 python3 tools/ab_summary.py $OUT/ab_cave.jsonl
+# bounce-batch threshold re-sweep with the sky items out of the fused loop (HRT_OPT_SECONDARY_BATCH)
+for r in 1 2; do for sb in 20 28 36 44 52; do
+  out=$(timeout -k 10 120 python3 tools/frames.py --batch 20 --frames 3 --sec-batch $sb 2>&1 | tail -1) || { echo "sweep failed: $out"; exit 1; }
+  echo "{\"round\": $r, \"sec_batch\": $sb, \"result\": $out}"
+done; done > $OUT/sec_batch_island.jsonl
+python3 -c "
+import json,collections
+b=collections.defaultdict(list)
+for l in open('$OUT/sec_batch_island.jsonl'): d=json.loads(l); b[d['sec_batch']].append(min(d['result']['ms']))
+print('sec_batch', {k: round(min(v),3) for k,v in b.items()})"
