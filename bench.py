@@ -357,6 +357,7 @@ def main():
                                       f"{', then the row-tile gather' if dist_on else ''})" if fpl > 1 else
                                       f"(trace + accumulate{' + row-tile gather' if dist_on else ''} per frame)"),
                        "frames_per_launch": fpl if fpl > 1 else 1,
+                       "launch_frames": int(st.last_frames),  # the timed launches' frames, as the library split them
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                        "parallelism": (f"row-tiles{world}x{args.row_tile} (" +
                                        ("RCCL ncclGather behind hrt_read_image" if lib_gather else "gloo all-gather")

@@ -23,7 +23,8 @@ for line in open(sys.argv[1]):
     if line.startswith("{"):
         c = json.loads(line)["config"]
         steps = json.loads(line)["steps"]
-        c["frames_per_launch"] = min(c["frames_per_launch"], steps)  # the timed launch's frames
+        # the timed launch's frames as the library split the steps (hrt_stats.last_frames)
+        c["frames_per_launch"] = c.get("launch_frames") or min(c["frames_per_launch"], steps)
         print(" ".join(f"{k}={c[k]}" for k in ("scene", "width", "height", "spp", "bounces", "kernel_variant",
                                                  "frames_per_launch")), c["frames_per_launch"])
 PY
