@@ -928,8 +928,9 @@ __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool a
 
 // Primary segments from the wave's list (ALL 64 lanes active).  Per lane: spheres, the meshes' AABB
 // quirk (raytracing.glsl:279) and its test count, then the listed triangles in buffer order.
-__device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParams& P, const TileList& tl, bool prim,
-                                               f3 o, f3 d, uint32_t& tests, Closest& c) {
+// Returns the entries it tested (the others: no primary lane's mesh vote or lane mask; diagnostics).
+__device__ __forceinline__ uint32_t world_hit_tile(const Scene& sc, const TraceParams& P, const TileList& tl, bool prim,
+                                                   f3 o, f3 d, uint32_t& tests, Closest& c) {
   const hrt_push_constants& pc = P.pc;
   spheres_first(sc, pc, prim, o, d, c);
   // primary lanes start at cam_pos (the table's origin): bit 8m of pm is mesh m's AABB test, by the
@@ -962,11 +963,13 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
   // (the list length through readfirstlane: hipcc had lost its uniformity through build_tile_list's
   // early returns and ran the entry loop as a divergent loop with a VGPR trip count)
   const uint32_t n = HRT_LIST_UNIFORM ? __builtin_amdgcn_readfirstlane(tl.n) : tl.n;
+  uint32_t tested = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t e = entry(i);
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
     const bool pass = prim && ((pm >> (8 * m)) & 1ull) && ((tl.lmask >> i) & 1ull);
     if (!__any(pass)) continue;
+    ++tested;
     {
     // the whole record in one load: the exact test's operands arrive with the normal (one K$ round
     // trip per entry instead of two dependent ones)
@@ -977,6 +980,7 @@ __device__ __forceinline__ void world_hit_tile(const Scene& sc, const TraceParam
                         make_float4(R[8], R[9], R[10], R[11]), dn, d, m, c, best_k);
     }
   }
+  return tested;
 }
 
 // Primary segments of the lanes with prim == true.  Called with ALL 64 lanes of the wave active.
@@ -2262,10 +2266,10 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     if (co.w == 0) co.work += 2u + (any_prim ? 1u + (tl.ok ? tl.n : 64u) : 0u);  // shading, primary list
     if (any_prim) {
       if (tl.ok) {
-        world_hit_tile(HRT_SHADE_KARGS ? kscene() : sc, P, tl, prim, p.pos, p.dir, tests, c);
+        const uint32_t tested = world_hit_tile(HRT_SHADE_KARGS ? kscene() : sc, P, tl, prim, p.pos, p.dir, tests, c);
         if (D && P.diag) {
           dg.prim_considered += tl.n;
-          dg.prim_survivors += tl.n;
+          dg.prim_survivors += tested;
         }
       } else {
         world_hit_bundle<D>(sc, P, prim, p.pos, p.dir, tests, c, dg);

@@ -21,3 +21,5 @@ import json,collections
 b=collections.defaultdict(list)
 for l in open('$OUT/sec_batch_island.jsonl'): d=json.loads(l); b[d['sec_batch']].append(min(d['result']['ms']))
 print('sec_batch', {k: round(min(v),3) for k,v in b.items()})"
+SKIP_TESTS=1 DIAG=1 bash tools/r04.sh r04d || exit 1
+grep -h primary_iters $OUT/diag_island.jsonl $OUT/diag_cave.jsonl | python3 -c "import sys,json; [print('list entries tested: %.3f of %.2f per primary iteration' % (d['primary_survival'], d['primary_list_len'])) for d in map(json.loads, sys.stdin)]"
