@@ -831,7 +831,8 @@ __device__ __forceinline__ Bundle tile_bundle(const hrt_push_constants& pc, bool
   b.c_lo = wave_min_all(lam) - 1e-5f;
   b.c_hi = 1.00001f;
   b.s_hi = __builtin_sqrtf(fmaxf(0.0f, 1.00002f - b.c_lo * b.c_lo)) * 1.00001f + 1e-6f;
-  ok = b.c_lo > 0.5f;  // a sane cap (NaN -> false)
+  // a sane cap (NaN -> false; fminf skips a NaN corner, so a corner that overflowed is checked here)
+  ok = b.c_lo > 0.5f && !__any(!(lam == lam));
   return b;
 }
 
@@ -866,13 +867,17 @@ __device__ __forceinline__ unsigned long long lane_list_mask(const TraceParams& 
   Bundle b;
   b.a = dir(centre);
   float lam = 3.0f;
+  bool nan = false;
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    lam = fminf(lam, dot(dir(mk(centre.x, centre.y + ((k & 1) ? j : -j), centre.z + ((k & 2) ? j : -j))), b.a));
+  for (int k = 0; k < 4; ++k) {
+    const float x = dot(dir(mk(centre.x, centre.y + ((k & 1) ? j : -j), centre.z + ((k & 2) ? j : -j))), b.a);
+    nan |= !(x == x);
+    lam = fminf(lam, x);
+  }
   b.c_lo = lam - 1e-5f;
   b.c_hi = 1.00001f;
   b.s_hi = __builtin_sqrtf(fmaxf(0.0f, 1.00002f - b.c_lo * b.c_lo)) * 1.00001f + 1e-6f;
-  const bool ok = active && b.c_lo > 0.5f;  // (NaN -> false)
+  const bool ok = active && !nan && b.c_lo > 0.5f;  // (NaN axis -> c_lo NaN -> false)
   const float4* cam_cull = kargs()->cam_cull;
   unsigned long long mask = 0ull;
   for (uint32_t i = 0, n = __builtin_amdgcn_readfirstlane(t.n); i < n; ++i) {
