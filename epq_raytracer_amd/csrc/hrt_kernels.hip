@@ -853,7 +853,8 @@ __device__ __forceinline__ bool bundle_keep(const float4* __restrict__ cr, uint3
 // an entry that no primary lane of the iteration can accept.  A pixel's cap covers ~1/64 of the
 // tile's, so it meets fewer of the list's triangles.  NaN or a cap over 60 degrees: every bit set.
 #ifndef HRT_LANE_MASK
-#define HRT_LANE_MASK 1
+#define HRT_LANE_MASK 0  // (r04d: a pixel's cap still meets 87% of its tile's entries on island; 1.869 -> 1.859 ms
+                         // island but 5.694 -> 5.717 cave, +16 B scratch: off)
 #endif
 __device__ __forceinline__ unsigned long long lane_list_mask(const TraceParams& P, const TileList& t, bool active,
                                                              f3 centre) {
@@ -2241,20 +2242,10 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     const bool ready = !done && p.bounce == 0;  // a primary segment to run
     const bool waiting = !done && p.bounce != 0;
     const uint32_t nwait = (uint32_t)__popcll(__ballot(waiting));
-#ifndef HRT_PRIM_BATCH
-#define HRT_PRIM_BATCH 0
-#endif
-#if HRT_PRIM_BATCH
-    // (A/B) primary segments wait too while a bounce batch runs and fewer than HRT_PRIM_BATCH lanes
-    // have one: the list loop's cost is per wave, not per lane.  Every iteration still runs one phase.
-    const uint32_t nready = (uint32_t)__popcll(__ballot(ready));
-    const bool run_prim = nready > 0 && (nready >= HRT_PRIM_BATCH || nwait < sec_thresh);
-    const bool prim = ready && run_prim;
-    const bool any_prim = run_prim;
-#else
+    // (r04d, measured and dropped: primary segments waiting too while a bounce batch runs and fewer than
+    // 8 lanes have one -- island 1.859 -> 1.878 ms)
     const bool prim = ready;
     const bool any_prim = __any(prim);
-#endif
     const bool run_sec = nwait > 0 && (nwait >= sec_thresh || !any_prim);
     const bool sec = waiting && run_sec;
     Closest c{kFltMax, 0, 0u, 0u};
