@@ -776,7 +776,6 @@ struct TileList {
   unsigned long long aabb;
   bool aabb_ok;
   uint32_t tsum;  // lane l: the triangle tests of a primary ray in octant l & 7 (sum of passing meshes' len)
-  unsigned long long lmask;  // per lane: bit i clear = entry i is outside this lane's own cap (lane_list_mask)
 };
 
 // intersecting_aabb's result for origin o depends only on the signs of (bound - o) and of 1/d per
@@ -846,52 +845,10 @@ __device__ __forceinline__ bool bundle_keep(const float4* __restrict__ cr, uint3
   return !rej;
 }
 
-// Per-lane refinement of a VGPR list (<= 64 entries): the cap of the lane's OWN primary directions --
-// its centre + (0, [-j, j], [-j, j]), the tile cap's construction for a single centre -- against each
-// entry's bundle-cull records.  Bit i clear proves the lane's primaries cannot accept entry i (the
-// bundle rules are exact rejections over any cap containing the directions), so world_hit_tile skips
-// an entry that no primary lane of the iteration can accept.  A pixel's cap covers ~1/64 of the
-// tile's, so it meets fewer of the list's triangles.  NaN or a cap over 60 degrees: every bit set.
-#ifndef HRT_LANE_MASK
-#define HRT_LANE_MASK 0  // (r04d: a pixel's cap still meets 87% of its tile's entries on island; 1.869 -> 1.859 ms
-                         // island but 5.694 -> 5.717 cave, +16 B scratch: off)
-#endif
-__device__ __forceinline__ unsigned long long lane_list_mask(const TraceParams& P, const TileList& t, bool active,
-                                                             f3 centre) {
-  const hrt_push_constants& pc = P.pc;
-  const float j = fabsf(pc.jitter_size) * 1.0001f;
-  const float* M = pc.cam_alignment_mat;
-  auto dir = [&](f3 v) {
-    return normalize(mk(M[0] * v.x + M[4] * v.y + M[8] * v.z, M[1] * v.x + M[5] * v.y + M[9] * v.z,
-                        M[2] * v.x + M[6] * v.y + M[10] * v.z));
-  };
-  Bundle b;
-  b.a = dir(centre);
-  float lam = 3.0f;
-  bool nan = false;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float x = dot(dir(mk(centre.x, centre.y + ((k & 1) ? j : -j), centre.z + ((k & 2) ? j : -j))), b.a);
-    nan |= !(x == x);
-    lam = fminf(lam, x);
-  }
-  b.c_lo = lam - 1e-5f;
-  b.c_hi = 1.00001f;
-  b.s_hi = __builtin_sqrtf(fmaxf(0.0f, 1.00002f - b.c_lo * b.c_lo)) * 1.00001f + 1e-6f;
-  const bool ok = active && !nan && b.c_lo > 0.5f;  // (NaN axis -> c_lo NaN -> false)
-  const float4* cam_cull = kargs()->cam_cull;
-  unsigned long long mask = 0ull;
-  for (uint32_t i = 0, n = __builtin_amdgcn_readfirstlane(t.n); i < n; ++i) {
-    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)t.v, (int)i) & 0x07FFFFFFu;
-    if (!ok || bundle_keep(cam_cull, k, b)) mask |= 1ull << i;
-  }
-  return mask;
-}
-
 // Builds the wave's list (all 64 lanes active; the caller synchronises before reading it).
 __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool active, f3 centre, uint32_t* lds) {
   const hrt_push_constants& pc = P.pc;
-  TileList t{0u, lds, 0u, false, 0ull, false, 0u, ~0ull};
+  TileList t{0u, lds, 0u, false, 0ull, false, 0u};
   const uint32_t cap = lds ? kTileCapLds : kTileCapVgpr;
   if (pc.num_meshes > 32 || !__any(active)) return t;
   bool ok;
@@ -926,15 +883,12 @@ __device__ __forceinline__ TileList build_tile_list(const TraceParams& P, bool a
   }
   t.ok = true;
   wave_handoff();  // the list's entries (other lanes' stores) before the reads of world_hit_tile
-#if HRT_LANE_MASK
-  if (!lds && t.n > 0u) t.lmask = lane_list_mask(P, t, active, centre);
-#endif
   return t;
 }
 
 // Primary segments from the wave's list (ALL 64 lanes active).  Per lane: spheres, the meshes' AABB
 // quirk (raytracing.glsl:279) and its test count, then the listed triangles in buffer order.
-// Returns the entries it tested (the others: no primary lane's mesh vote or lane mask; diagnostics).
+// Returns the entries it tested (the others: no primary lane's mesh vote; diagnostics).
 __device__ __forceinline__ uint32_t world_hit_tile(const Scene& sc, const TraceParams& P, const TileList& tl, bool prim,
                                                    f3 o, f3 d, uint32_t& tests, Closest& c) {
   const hrt_push_constants& pc = P.pc;
@@ -973,7 +927,7 @@ __device__ __forceinline__ uint32_t world_hit_tile(const Scene& sc, const TraceP
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t e = entry(i);
     const uint32_t kk = e & 0x07FFFFFFu, m = e >> 27;
-    const bool pass = prim && ((pm >> (8 * m)) & 1ull) && ((tl.lmask >> i) & 1ull);
+    const bool pass = prim && ((pm >> (8 * m)) & 1ull);
     if (!__any(pass)) continue;
     ++tested;
     {
