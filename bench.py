@@ -145,8 +145,10 @@ def spawn_ranks(n: int, argv, cmd=None, poll_s: float = 0.1) -> int:
 def rank_record(ctx, rank, world, lib_gather, kern_ms, gather_ms, segs) -> dict:
     """What one rank reports to rank 0 for an N > 1 line: the communicator the LIBRARY has
     (hrt_comm_info: did RCCL see N ranks?), its per-frame kernel time and its gather's wall time."""
-    crank, cworld, transport = ctx.comm_info() if lib_gather else (rank, world, 0)
-    return {"rank": rank, "rccl_rank": int(crank), "rccl_world": int(cworld), "transport": int(transport),
+    # (no library communicator on the gloo rehearsal: the rccl fields are null there)
+    crank, cworld, transport = ctx.comm_info() if lib_gather else (None, None, 0)
+    return {"rank": rank, "rccl_rank": None if crank is None else int(crank),
+            "rccl_world": None if cworld is None else int(cworld), "transport": int(transport),
             "kernel_ms": round(float(kern_ms), 4), "gather_ms": None if gather_ms is None else round(gather_ms, 4),
             "segments": int(segs)}
 
@@ -156,13 +158,14 @@ def assemble_ranks(recs: list, world: int) -> dict:
     communicator's world size as the ranks see it (min / max: 8 and 8 when RCCL joined all 8), the rank
     ids it gave them, each rank's kernel time and gather time (max = what the step waited for)."""
     recs = sorted(recs, key=lambda r: r["rank"])
-    worlds = [r["rccl_world"] for r in recs]
+    worlds = [r["rccl_world"] for r in recs if r["rccl_world"] is not None]
     gms = [r["gather_ms"] for r in recs if r["gather_ms"] is not None]
+    rccl = len(worlds) == len(recs)  # every rank joined a library communicator (not the gloo rehearsal)
     return {"reported": len(recs), "world": world,
-            "rccl_world": {"min": min(worlds), "max": max(worlds)},
-            "rccl_ranks": [r["rccl_rank"] for r in recs],
-            "rccl_ok": len(recs) == world and min(worlds) == max(worlds) == world
-                       and sorted(r["rccl_rank"] for r in recs) == list(range(world)),
+            "rccl_world": {"min": min(worlds), "max": max(worlds)} if rccl else None,
+            "rccl_ranks": [r["rccl_rank"] for r in recs] if rccl else None,
+            "rccl_ok": (len(recs) == world and min(worlds) == max(worlds) == world
+                        and sorted(r["rccl_rank"] for r in recs) == list(range(world))) if rccl else None,
             "transport": sorted({r["transport"] for r in recs}),
             "kernel_ms": [r["kernel_ms"] for r in recs],
             "kernel_ms_max": max(r["kernel_ms"] for r in recs),

@@ -104,3 +104,11 @@ def test_rank_records_reach_rank_0_over_gloo(tmp_path):
     got = json.loads(out.read_text())
     assert got["rccl_ok"] and got["rccl_world"] == {"min": 2, "max": 2} and got["rccl_ranks"] == [0, 1]
     assert got["kernel_ms"] == [0.5, 1.5] and got["gather_ms"] == [2.0, 4.0] and got["gather_ms_max"] == 4.0
+
+
+def test_gloo_rehearsal_has_no_rccl_claims():
+    recs = [{"rank": r, "rccl_rank": None, "rccl_world": None, "transport": 0, "kernel_ms": 1.0, "gather_ms": 4.0,
+             "segments": 10} for r in range(2)]
+    got = bench.assemble_ranks(recs, 2)
+    assert got["rccl_ok"] is None and got["rccl_world"] is None and got["rccl_ranks"] is None
+    assert got["gather_ms_max"] == 4.0 and got["reported"] == 2
