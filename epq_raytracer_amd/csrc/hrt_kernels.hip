@@ -1429,6 +1429,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_MIXED
 #define HRT_WQ_MIXED 1   // short node and triangle stacks share one step
 #endif
+#ifndef HRT_WQ_EARLY_REC
+#define HRT_WQ_EARLY_REC 1  // a node step's first member pair read before the slot read (r04)
+#endif
 #ifndef HRT_WQ_TRI_MIN
 #define HRT_WQ_TRI_MIN 64u  // a triangle step runs once this many triangle pairs wait (or no node pair is left)
 #endif
@@ -1900,6 +1903,14 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     if (is_node) {
       const uint32_t g = e >> 6, fc = g & 0xFFFFu, gcnt = (g >> 16) + 1u;
       if (!overflow) {
+#if HRT_WQ_EARLY_REC
+        // the first member pair's records are requested before the slot read: that read is an atomic
+        // (lds_get), which the scheduler keeps every other memory access on its side of, so requested
+        // after it they waited for the ray shuffles and the slot before being issued
+        const float4* na0 = wq.nodes + 3 * fc;
+        const float4* nb0 = wq.nodes + 3 * (fc + min(1u, gcnt - 1u));
+        const float4 A00 = na0[0], A01 = na0[1], A02 = na0[2], B00 = nb0[0], B01 = nb0[1], B02 = nb0[2];
+#endif
         const float t_hi = wq_slot_t(wq, r) * (1.0f + rel_t) + rabs;
         auto member = [&](const float4& N0, const float4& N1, const float4& N2, int k, bool valid = true) {
           float tnear;
@@ -1929,6 +1940,13 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         // (A/B) every slot tested, the ones past the group's count masked (no per-pair branch)
 #pragma unroll
         for (int h = 0; h < (int)kWqSlots / 2; ++h) {
+#if HRT_WQ_EARLY_REC
+          if (h == 0) {
+            member(A00, A01, A02, 0);
+            member(B00, B01, B02, 1);
+            continue;
+          }
+#endif
           const float4* na = wq.nodes + 3 * (fc + min(2u * h, gcnt - 1u));
           const float4* nb = wq.nodes + 3 * (fc + min(2u * h + 1u, gcnt - 1u));
           const float4 A0 = na[0], A1 = na[1], A2 = na[2], B0 = nb[0], B1 = nb[1], B2 = nb[2];
