@@ -2078,6 +2078,9 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #ifndef HRT_SKY_LOOP
 #define HRT_SKY_LOOP 1
 #endif
+#ifndef HRT_SKY_UNROLL
+#define HRT_SKY_UNROLL 2  // samples per trip of the sky loop
+#endif
 template <bool Zero>
 __device__ __forceinline__ void sky_segment(const KArgs K, const TileList& tl, bool active, f3 centre, uint32_t& state,
                                             f3& colour, uint32_t& tests) {
@@ -2110,17 +2113,17 @@ __device__ __forceinline__ void sky_samples(const TileList& tl, bool active, f3 
   if (HRT_SKY_ZERO && fabsf(K->pc.jitter_size) < __builtin_inff() &&
       __all(!active || (centre.x != 0.0f && centre.y != 0.0f && fabsf(centre.x) < __builtin_inff() &&
                         fabsf(centre.y) < __builtin_inff()))) {  // get_ray_dir_sky<true>'s premises
-    for (; s + 2 <= ns; s += 2) {
-      sky_segment<true>(K, tl, active, centre, state, colour, t);
-      sky_segment<true>(K, tl, active, centre, state, colour, t);
+    for (; s + HRT_SKY_UNROLL <= ns; s += HRT_SKY_UNROLL) {
+#pragma unroll
+      for (int u = 0; u < HRT_SKY_UNROLL; ++u) sky_segment<true>(K, tl, active, centre, state, colour, t);
     }
-    if (s < ns) sky_segment<true>(K, tl, active, centre, state, colour, t);
+    for (; s < ns; ++s) sky_segment<true>(K, tl, active, centre, state, colour, t);
   } else {
-    for (; s + 2 <= ns; s += 2) {
-      sky_segment<false>(K, tl, active, centre, state, colour, t);
-      sky_segment<false>(K, tl, active, centre, state, colour, t);
+    for (; s + HRT_SKY_UNROLL <= ns; s += HRT_SKY_UNROLL) {
+#pragma unroll
+      for (int u = 0; u < HRT_SKY_UNROLL; ++u) sky_segment<false>(K, tl, active, centre, state, colour, t);
     }
-    if (s < ns) sky_segment<false>(K, tl, active, centre, state, colour, t);
+    for (; s < ns; ++s) sky_segment<false>(K, tl, active, centre, state, colour, t);
   }
   if (active) {
     segs += ns > 0 ? (uint32_t)ns : 0u;
