@@ -2079,7 +2079,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #define HRT_SKY_LOOP 1
 #endif
 #ifndef HRT_SKY_UNROLL
-#define HRT_SKY_UNROLL 2  // samples per trip of the sky loop
+#define HRT_SKY_UNROLL 1  // samples per trip of the sky loop (r04i/j: 1 beats 2 by ~1% on island; 3, 4 no better)
 #endif
 template <bool Zero>
 __device__ __forceinline__ void sky_segment(const KArgs K, const TileList& tl, bool active, f3 centre, uint32_t& state,
