@@ -1910,6 +1910,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
         const float4* na0 = wq.nodes + 3 * fc;
         const float4* nb0 = wq.nodes + 3 * (fc + min(1u, gcnt - 1u));
         const float4 A00 = na0[0], A01 = na0[1], A02 = na0[2], B00 = nb0[0], B01 = nb0[1], B02 = nb0[2];
+        // (both pairs up front: 24 more live VGPRs, scratch 92 -> 160 B with spills in the fused loop)
 #endif
         const float t_hi = wq_slot_t(wq, r) * (1.0f + rel_t) + rabs;
         auto member = [&](const float4& N0, const float4& N1, const float4& N2, int k, bool valid = true) {
