@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--busy-split", type=int, nargs="+", default=[2], help="HRT_OPT_BUSY_SPLIT values")
     ap.add_argument("--defer", type=int, nargs="+", default=[1], help="HRT_OPT_DEFER_COMBINE values")
+    ap.add_argument("--no-accumulate", action="store_true",
+                    help="traces only (the combine's cost and its waits left out: a lower bound)")
     ap.add_argument("--grid-cus", type=int, nargs="+", default=[0],
                     help="HRT_OPT_GRID_CUS values (libhip_raytrace_debug.so; 0 = every CU)")
     a = ap.parse_args()
@@ -50,12 +52,13 @@ def main():
             t0 = time.perf_counter()
             for _ in range(a.frames):
                 ctx.trace(case.push(k))
-                ctx.accumulate(k)
+                if not a.no_accumulate:
+                    ctx.accumulate(k)
                 k += 1
             ctx.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / a.frames
             print(json.dumps({"round": r, "lanes": lanes, "grid_cus": cus, "busy_split": bs, "defer": df,
-                              "ms_per_frame": round(ms, 3)}), flush=True)
+                              "accumulate": not a.no_accumulate, "ms_per_frame": round(ms, 3)}), flush=True)
         if debug:
             ctx.set_option(_lib.OPT_GRID_CUS, 0)
         ctx.synchronize()
