@@ -109,7 +109,8 @@ __device__ __forceinline__ uint32_t global_row(uint32_t lr, const TraceParams& /
 // get_ray_dir, raytracing.glsl:162-166 (u1, u2, u3 in that order)
 template <class PC>
 __device__ __forceinline__ f3 get_ray_dir(const PC& pc, f3 c, uint32_t& state) {
-  const float r = (u01(hash(state)) * 2.0f) * 3.14159265358979323846f;
+  // (u01 * 2) * pi: the doubling is exact too, so one multiply by pi 2^-31 (u01_mul)
+  const float r = u01_mul(hash(state), 3.14159265358979323846f * 0x1p-31f);
   float sr, cr;
   spec_sincos_angle(r, sr, cr);  // r in [0, 2pi]
   // (r03, measured slower: the zero components of t1 / t2 as signed zeros -- 4.5 M fewer VALU per
@@ -125,7 +126,7 @@ __device__ __forceinline__ f3 get_ray_dir(const PC& pc, f3 c, uint32_t& state) {
   const f3 w = mk(__builtin_fmaf(M[8], nc.z, __builtin_fmaf(M[4], nc.y, M[0] * nc.x)),
                   __builtin_fmaf(M[9], nc.z, __builtin_fmaf(M[5], nc.y, M[1] * nc.x)),
                   __builtin_fmaf(M[10], nc.z, __builtin_fmaf(M[6], nc.y, M[2] * nc.x)));
-  return normalize(w);
+  return normalize_fl(w);
 }
 #ifndef HRT_NORM_UNIFORM
 #define HRT_NORM_UNIFORM 1  // (r04b: with HRT_SKY_ZERO island 1.903 -> 1.876 ms per frame)
@@ -143,7 +144,7 @@ template <bool Zero, class PC>
 __device__ __forceinline__ f3 get_ray_dir_sky(const PC& pc, f3 c, uint32_t& state) {
   if constexpr (!Zero) {
 #if HRT_NORM_UNIFORM
-    const float r = (u01(hash(state)) * 2.0f) * 3.14159265358979323846f;
+    const float r = u01_mul(hash(state), 3.14159265358979323846f * 0x1p-31f);  // (u01 * 2) * pi
     float sr, cr;
     spec_sincos_angle(r, sr, cr);
     const float j = pc.jitter_size;
@@ -160,7 +161,7 @@ __device__ __forceinline__ f3 get_ray_dir_sky(const PC& pc, f3 c, uint32_t& stat
     return get_ray_dir(pc, c, state);
 #endif
   } else {
-    const float r = (u01(hash(state)) * 2.0f) * 3.14159265358979323846f;
+    const float r = u01_mul(hash(state), 3.14159265358979323846f * 0x1p-31f);  // (u01 * 2) * pi
     float sr, cr;
     spec_sincos_angle(r, sr, cr);
     const float j = pc.jitter_size;
@@ -292,7 +293,7 @@ __device__ __forceinline__ f3 environment_light(const PC& pc, f3 d) {
 #define HRT_FUZZ_INT 1  // the fast path's radius test on the hash bits (r03ai)
 #endif
 __device__ __forceinline__ f3 adjust_dir(f3 d, f3 n, const hrt_material& mat, bool specular, uint32_t& state) {
-  const f3 diffuse_dir = normalize(n + unit_sphere(state));
+  const f3 diffuse_dir = normalize_fl(n + unit_sphere(state));
   const float k = 2.0f * dot(n, d);
   const f3 specular_dir = d - n * k;
   const float a = mat.settings[1] * (float)(int)specular;
@@ -328,13 +329,13 @@ __device__ __forceinline__ f3 adjust_dir(f3 d, f3 n, const hrt_material& mat, bo
                        fabsf(specular_dir.z) < __builtin_inff();
   if (fast && finite_nz && spec_ok) {
     state = st;
-    return normalize(diffuse_dir);
+    return normalize_fl(diffuse_dir);
   }
 #endif
   const f3 fuzz = unit_sphere(state) * mat.settings[2];
   const f3 mixed = mk(diffuse_dir.x * oma + specular_dir.x * a, diffuse_dir.y * oma + specular_dir.y * a,
                       diffuse_dir.z * oma + specular_dir.z * a);
-  return normalize(mixed + fuzz);
+  return normalize_fl(mixed + fuzz);
 }
 
 // Per-lane path state of trace_ray (raytracing.glsl:308-352).
@@ -2087,20 +2088,27 @@ __device__ __forceinline__ void sky_segment(const KArgs K, const TileList& tl, b
                                             f3& colour, uint32_t& tests) {
   const auto& pc = K->pc;
   const f3 dir = get_ray_dir_sky<Zero>(pc, centre, state);
-  const f3 d = HRT_NORM_UNIFORM ? normalize_wu(dir) : normalize(dir);
+  // unit: the wave's second normalize took its fast path, so |d.c| <= 1 + 2^-23 in every lane (normalize_wu)
+  bool unit = false;
+  const f3 d = HRT_NORM_UNIFORM ? normalize_wu(dir, unit) : normalize(dir);
   // world_hit_tile's test count: the octant table (one lane read, all 64 lanes run this), or the
-  // literal AABB test off its domain
-  const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
-  const uint32_t oct_tests = (uint32_t)__shfl((int)tl.tsum, (int)oct, 64);
-  if (__builtin_expect(tl.aabb_ok && fabsf(d.x) <= 1.5f && fabsf(d.y) <= 1.5f && fabsf(d.z) <= 1.5f, 1)) {
+  // literal AABB test off its domain (|d.c| <= 1.5: implied by unit)
+  // (the octant's byte address for ds_bpermute directly: __shfl added the lane's 64-lane segment base)
+  const uint32_t oct4 = ((fbits(d.x) >> 31) << 2) | ((fbits(d.y) >> 31) << 3) | ((fbits(d.z) >> 31) << 4);
+  const uint32_t oct_tests = (uint32_t)__builtin_amdgcn_ds_bpermute((int)oct4, (int)tl.tsum);
+  if (__builtin_expect(tl.aabb_ok && (unit || (fabsf(d.x) <= 1.5f && fabsf(d.y) <= 1.5f && fabsf(d.z) <= 1.5f)), 1)) {
     tests += oct_tests;
   } else if (active) {
     const f3 o = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
     for (int m = 0; m < pc.num_meshes; ++m)
       if (aabb_pass(K->meshes[m], o, d)) tests += K->meshes[m].len;
   }
-  // shade_step's miss (p.light = 0 + environment light) and the caller's colour += light * (1, 1, 1)
-  const f3 light = mk(0.0f, 0.0f, 0.0f) + environment_light(pc, d);
+  // shade_step's miss (p.light = 0 + environment light) and the caller's colour += light * (1, 1, 1).
+  // With |d.y| <= 1 + 2^-23 each light component is (1 - a) + a k with a = (d.y + 1) / 2 in
+  // [-2^-24, 1 + 2^-24] and k in [0.5, 1]: at least 0.5 - 2^-23, never a zero, so 0 + light == light
+  // (and without the environment light it is +0 either way).
+  f3 light = environment_light(pc, d);
+  if (!unit) light = mk(0.0f, 0.0f, 0.0f) + light;
   colour = colour + light * mk(1.0f, 1.0f, 1.0f);
 }
 // The lanes' whole pixels.  ALL 64 lanes run it (wave-uniform condition; the idle lanes' results are
@@ -2208,10 +2216,10 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
         const KArgs K = kargs();
         const f3 dir = get_ray_dir(K->pc, centre, state);
         p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), mk(K->pc.cam_pos[0], K->pc.cam_pos[1], K->pc.cam_pos[2]),
-                 normalize(dir), 0, true};
+                 normalize_fl(dir), 0, true};
 #else
         const f3 dir = get_ray_dir(pc, centre, state);
-        p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, normalize(dir), 0, true};
+        p = Path{mk(0.0f, 0.0f, 0.0f), mk(1.0f, 1.0f, 1.0f), root, normalize_fl(dir), 0, true};
 #endif
       }
     }

@@ -104,17 +104,31 @@ __device__ __forceinline__ f3 normalize(f3 a) {
 // case for ray directions) the wave runs it without the per-lane exec-mask split around the IEEE
 // fallback (which every lane then skips); otherwise every active lane runs the IEEE spelling, which
 // is exact everywhere.  Same bits as normalize either way.
-__device__ __forceinline__ f3 normalize_wu(f3 a) {
+// fast: the wave took the fast path (then every active lane's result has |component| <= 1 + 2^-23:
+// |a.c| <= sqrt(RN dot) (1 + 2^-24) and the quotient is correctly rounded)
+__device__ __forceinline__ f3 normalize_wu(f3 a, bool& fast_all) {
   const float d2 = dot(a, a);
   const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
-  const bool fast = d2 >= 0x1p-80f && d2 <= 0x1p78f && m >= 0x1p-80f;
-  if (__builtin_expect(__all(fast), 1)) {
+  // (a ballot per compare: each is the compare's own lane mask, no VGPR round trip)
+  fast_all = (__builtin_amdgcn_ballot_w64(d2 >= 0x1p-80f) & __builtin_amdgcn_ballot_w64(d2 <= 0x1p78f) &
+              __builtin_amdgcn_ballot_w64(m >= 0x1p-80f)) == __builtin_amdgcn_read_exec();
+  if (__builtin_expect(fast_all, 1)) {
     const float l = sqrt_core(d2);
     const float y = rcp_core(l);
     return {div_core(a.x, l, y), div_core(a.y, l, y), div_core(a.z, l, y)};
   }
   return a / __builtin_sqrtf(d2);
 }
+__device__ __forceinline__ f3 normalize_wu(f3 a) {
+  bool f;
+  return normalize_wu(a, f);
+}
+// The fused loop's and the shading's normalizes (ray generation, adjust_dir, unit_sphere): per wave
+// (normalize_wu) or per lane (normalize); the same bits either way.
+#ifndef HRT_NORM_UNIFORM_FUSED
+#define HRT_NORM_UNIFORM_FUSED 1  // (r04r: island 1.843 -> 1.838, cave 5.625 -> 5.601 ms per frame)
+#endif
+__device__ __forceinline__ f3 normalize_fl(f3 a) { return HRT_NORM_UNIFORM_FUSED ? normalize_wu(a) : normalize(a); }
 // The reference's spelling of both (for the self-check).
 __device__ __forceinline__ f3 normalize_ieee(f3 a) { return a / __builtin_sqrtf(dot(a, a)); }
 // S6: GLSL 4.60 definitions.
@@ -259,6 +273,9 @@ __device__ __forceinline__ uint32_t hash(uint32_t& state) {  // :13-21
 }
 // scaleToRange01 :23-25 -- float(4294967295.0) == 2^32, so the divide is an exact power-of-two scale.
 __device__ __forceinline__ float u01(uint32_t s) { return (float)s * 2.3283064365386963e-10f; }
+// c * u01(s) in one multiply: u01's scaling by 2^-32 is exact (float(s) is 0 or >= 1), so
+// RN(c * (float(s) 2^-32)) == RN(float(s) * (c 2^-32)) with c 2^-32 an exact float (c_scaled)
+__device__ __forceinline__ float u01_mul(uint32_t s, float c_scaled) { return (float)s * c_scaled; }
 
 // sqrt on the RNG's values: sqrt_core is the correctly rounded sqrt on every u01 value (k * 2^-32, so 0
 // or >= 2^-32) and on every -2 log(u01) (0 .. 44.4, -0 at u = 1, +inf at u = 0): checked exhaustively
@@ -266,7 +283,7 @@ __device__ __forceinline__ float u01(uint32_t s) { return (float)s * 2.328306436
 __device__ __forceinline__ float sqrt_rng(float x) { return sqrt_core(x); }
 
 __device__ __forceinline__ float normal_dist(uint32_t& state) {  // :28-33
-  const float theta = 6.2831852f * u01(hash(state));  // 2 * 3.1415926 folded exactly
+  const float theta = u01_mul(hash(state), 6.2831852f * 0x1p-32f);  // 6.2831852f * u01: 2 * 3.1415926 folded exactly
   const float rho = sqrt_rng(-2.0f * spec_log_u01(u01(hash(state))));
   float s, c;
   spec_sincos_angle(theta, s, c);
@@ -276,7 +293,7 @@ __device__ __forceinline__ f3 unit_sphere(uint32_t& state) {  // :35-40
   const float x = normal_dist(state);
   const float y = normal_dist(state);
   const float z = normal_dist(state);
-  return normalize(mk(x, y, z));
+  return normalize_fl(mk(x, y, z));
 }
 
 // S7: R8G8B8A8_UNORM store / load.

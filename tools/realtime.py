@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--busy-split", type=int, nargs="+", default=[2], help="HRT_OPT_BUSY_SPLIT values")
     ap.add_argument("--defer", type=int, nargs="+", default=[1], help="HRT_OPT_DEFER_COMBINE values")
+    ap.add_argument("--split", type=int, nargs="+", default=[0], help="HRT_OPT_SPLIT values (0 = auto)")
+    ap.add_argument("--factor", type=int, nargs="+", default=[-1], help="HRT_OPT_SPLIT_FACTOR values (-1 = auto)")
     ap.add_argument("--no-accumulate", action="store_true",
                     help="traces only (the combine's cost and its waits left out: a lower bound)")
     ap.add_argument("--grid-cus", type=int, nargs="+", default=[0],
@@ -37,8 +39,11 @@ def main():
     ctx = case.context(debug=debug)
     k = 1
     for r in range(a.rounds):
-        for lanes, cus, bs, df in [(n, c, b, d) for n in a.lanes for c in a.grid_cus for b in a.busy_split
-                                   for d in a.defer]:
+        for lanes, cus, bs, df, sp, fc in [(n, c, b, d, sp, fc) for n in a.lanes for c in a.grid_cus
+                                           for b in a.busy_split for d in a.defer for sp in a.split
+                                           for fc in a.factor]:
+            ctx.set_option(_lib.OPT_SPLIT, sp)
+            ctx.set_option(_lib.OPT_SPLIT_FACTOR, fc)
             ctx.set_option(_lib.OPT_DEFER_COMBINE, df)
             ctx.set_option(_lib.OPT_OVERLAP, lanes)
             ctx.set_option(_lib.OPT_BUSY_SPLIT, bs)
@@ -58,9 +63,11 @@ def main():
             ctx.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / a.frames
             print(json.dumps({"round": r, "lanes": lanes, "grid_cus": cus, "busy_split": bs, "defer": df,
-                              "accumulate": not a.no_accumulate, "ms_per_frame": round(ms, 3)}), flush=True)
+                              "split": sp, "factor": fc, "accumulate": not a.no_accumulate, "ms_per_frame": round(ms, 3)}), flush=True)
         if debug:
             ctx.set_option(_lib.OPT_GRID_CUS, 0)
+        ctx.set_option(_lib.OPT_SPLIT, 0)
+        ctx.set_option(_lib.OPT_SPLIT_FACTOR, -1)
         ctx.synchronize()
         t0 = time.perf_counter()
         ctx.compute_n(case.push(k), a.frames)
