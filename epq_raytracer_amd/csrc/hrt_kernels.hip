@@ -71,6 +71,50 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
 
+// Exclusive prefix sum of x over the wave's 64 lanes in lane order, and the total (every lane active):
+// a Hillis-Steele scan inside each row of 16 lanes by DPP row shifts (lanes past a row's start read 0),
+// then each row adds the totals of the rows before it by the row broadcasts of lanes 15 and 31 -- six
+// adds with DPP operands instead of a ballot, two lane counts and a shift per bit of x.
+#ifndef HRT_DPP_SCAN
+#define HRT_DPP_SCAN 1
+#endif
+__device__ __forceinline__ uint32_t wave_scan_excl(uint32_t x, uint32_t& total, uint32_t bits = 32u) {
+#if HRT_DPP_SCAN
+  (void)bits;
+  // (inline: hipcc left each __builtin_amdgcn_mov_dpp as a separate move before a plain add.  Each step
+  // reads the previous one's result through DPP, which needs two wait states after a VALU write: the
+  // s_nops; in place, so the rows a broadcast's row mask leaves unwritten keep their value, i.e. add 0)
+  uint32_t v = x;
+  asm volatile(
+      "s_nop 1\n"
+      "v_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n"
+      "v_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+      "s_nop 1\n"
+      "v_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+      "s_nop 1\n"
+      : "+v"(v));
+  total = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  return v - x;
+#else
+  // bit-plane ballots: x < 2^bits
+  uint32_t pos = 0;
+  total = 0;
+  for (uint32_t b = 0; b < bits; ++b) {
+    const unsigned long long bb = __ballot((x >> b) & 1u);
+    pos += lanes_below(bb) << b;
+    total += (uint32_t)__popcll(bb) << b;
+  }
+  return pos;
+#endif
+}
+
 // Cross-lane handoffs through LDS (the pair stacks, the closest-hit slots, the band marks).  A lane's
 // store read by ANOTHER lane is a data exchange between threads, so it is written as one: relaxed
 // wavefront-scope atomics for the exchanged words and a wavefront-scope acquire-release fence between
@@ -1783,14 +1827,10 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       dg.band_len += n;
       band_lmax = n;
     }
-    // exclusive prefix pos of the lengths and their total from bit-plane ballots (no lane exchanges:
+    // exclusive prefix pos of the lengths and their total (wave_scan_excl; r03 used bit-plane ballots --
     // bvh_band_bits = the bit width of the scene's longest list; a 6-step shuffle scan was slower)
-    uint32_t pos = 0, total = 0;
-    for (uint32_t b = 0, nb = K->bvh_band_bits; b < nb; ++b) {
-      const unsigned long long bb = __ballot((n >> b) & 1u);
-      pos += lanes_below(bb) << b;
-      total += (uint32_t)__popcll(bb) << b;
-    }
+    uint32_t total;
+    const uint32_t pos = wave_scan_excl(n, total, K->bvh_band_bits);
     const void* band = K->bvh_band;
     const uint32_t wide = K->bvh_band_wide;
     const float4* nhat = K->bvh_band_nhat;
@@ -1848,13 +1888,8 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   if (rvis && rcnt == 0u) lds_put(&wq.ns[lanes_below(rb)], (rinfo << 6) | lane);  // inner root: its children's group
   uint32_t nc = (uint32_t)__popcll(rb);
   {  // leaf root (a scene of at most leaf-size triangles): its triangles, after any band pairs
-    uint32_t pre = tc, tot = 0;
-#pragma unroll
-    for (int b = 0; b < 5; ++b) {
-      const unsigned long long bb = __ballot((rcnt >> b) & 1u);
-      pre += lanes_below(bb) << b;
-      tot += (uint32_t)__popcll(bb) << b;
-    }
+    uint32_t tot;
+    const uint32_t pre = tc + wave_scan_excl(rcnt, tot, 5u);
     for (uint32_t j = 0; j < rcnt; ++j) lds_put(&wq.ts[pre + j], (((rinfo & 0x07FFFFFFu) + j) << 6) | lane);
     tc += tot;
   }
@@ -2004,17 +2039,12 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #endif
       nc += (uint32_t)__popcll(bk);
     }
-    // kept leaves' triangles: exclusive prefix of the per-lane counts (0..16) from bit-plane ballots
+    // kept leaves' triangles: exclusive prefix of the per-lane counts (0..16)
     uint32_t cnt = 0;
 #pragma unroll
     for (int k = 0; k < (int)kWqSlots; ++k) cnt += li[k] >> 27;
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int b = 0; b < 5; ++b) {
-      const unsigned long long bb = __ballot((cnt >> b) & 1u);
-      pre += lanes_below(bb) << b;
-      tot += (uint32_t)__popcll(bb) << b;
-    }
+    uint32_t tot;
+    const uint32_t pre = wave_scan_excl(cnt, tot, 5u);
     if (tc + tot <= tcap) {  // wave-uniform
       uint32_t at = tc + pre;
 #if HRT_WQ_LEAF_FLAT
@@ -2901,12 +2931,8 @@ __global__ __launch_bounds__(64) void band_flatten_check(const uint32_t* n_in, c
                                                          uint32_t* out) {
   __shared__ uint8_t marks[64];
   const uint32_t lane = threadIdx.x & 63u, n = n_in[lane], b0 = b0_in[lane];
-  uint32_t pos = 0, total = 0;
-  for (uint32_t b = 0; b < 32u; ++b) {
-    const unsigned long long bb = __ballot((n >> b) & 1u);
-    pos += lanes_below(bb) << b;
-    total += (uint32_t)__popcll(bb) << b;
-  }
+  uint32_t total;
+  const uint32_t pos = wave_scan_excl(n, total);  // (the kernel's scan, checked here on given counts)
   BandFlat bf{marks, lane, n, pos, total, b0 - pos, 0u};
   for (uint32_t r = 0; r < rounds; ++r) {
     uint32_t own;

@@ -1,0 +1,13 @@
+#!/bin/bash
+# r04s: exclusive prefix sums by a DPP row scan (wave_scan_excl) instead of bit-plane ballots: the
+# boundary tests (band flattening runs the same scan on given counts) and the parity suite on the new
+# in-tree build, then interleaved timing against the ballot build (ab_nodpp).
+set -o pipefail
+OUT=gpurun_out/r04s; mkdir -p $OUT
+B=epq_raytracer_amd/build
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_boundary.py tests/test_gpu_parity.py tests/test_gpu_configs.py -q -x --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+AB_BATCH=20 timeout -k 10 600 bash tools/ab.sh 3 $B/ab_nodpp/libhip_raytrace.so $B/ab_dpp/libhip_raytrace.so > $OUT/ab_island.jsonl 2>&1 || { echo "ab island failed"; tail -5 $OUT/ab_island.jsonl; exit 1; }
+python3 tools/ab_summary.py $OUT/ab_island.jsonl
+AB_BATCH=20 timeout -k 10 600 bash tools/ab.sh 3 $B/ab_nodpp/libhip_raytrace.so $B/ab_dpp/libhip_raytrace.so -- --scene cave --node-r 2 > $OUT/ab_cave.jsonl 2>&1 || { echo "ab cave failed"; tail -5 $OUT/ab_cave.jsonl; exit 1; }
+python3 tools/ab_summary.py $OUT/ab_cave.jsonl
