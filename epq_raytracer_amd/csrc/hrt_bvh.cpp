@@ -520,7 +520,7 @@ bool make_wq_nodes(const BvhHost& b, std::vector<float>& out, uint32_t width, ui
     uint32_t u[4];
     u[0] = h.conv(r[8], 0) | (uint32_t)h.conv(r[9], 0) << 16;
     u[1] = h.conv(r[10], 0) | (uint32_t)h.conv(r[11], -1) << 16;
-    u[2] = h.conv(r[12], +1) | esc_of[k] << 16;
+    u[2] = h.conv((double)r[12] * r[12] * 1.00001, +1) | esc_of[k] << 16;  // S >= sin^2 x 1.00001 (r[12] >= 0)
     u[3] = info_of[k];
     std::memcpy(&w[8], u, 16);
   }

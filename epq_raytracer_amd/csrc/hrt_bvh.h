@@ -110,7 +110,8 @@ constexpr uint64_t kBvhMaxEntries = 1u << 18;
 //   [0..2] box lo, [3] margin a, [4..6] box hi, [7] margin b   (the kept binary node's, unchanged)
 //   [8]  bits: cone axis x | axis y << 16   (binary16, nearest: |error| <= 2^-12 per component)
 //   [9]  bits: cone axis z | cos(phi) << 16 (cos rounded down)
-//   [10] bits: sin(phi) (rounded up) | escape << 16 (the next member of its group; the last member:
+//   [10] bits: S = sin(phi)^2 x 1.00001 (rounded up; the kernel's squared back-face test multiplies by it,
+//        the unsquared ones use sqrt(S)) | escape << 16 (the next member of its group; the last member:
 //        its parent's escape; root: the node count -- a stackless walk continues there after the subtree)
 //   [11] bits: leaf ? first_prim | count << 27 : fc | (group count - 1) << 16
 // The kernel widens its back-face cone test by the axis error, so the image only ever keeps more;

@@ -67,6 +67,19 @@ __device__ __forceinline__ Scene kscene() {
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 __device__ __forceinline__ f3 ray_at(f3 o, f3 d, float t) { return o + d * t; }  // :158-160
 
+// lane r's value (r < 64, every caller's index is a lane of this wave): ds_bpermute at r * 4 directly
+// (__shfl's width arithmetic added the lane's 64-lane segment base: two VALU per address)
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t r) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(r << 2), (int)v);
+}
+__device__ __forceinline__ float lane_read(float v, uint32_t r) {
+  return __uint_as_float(lane_read(__float_as_uint(v), r));
+}
+// ray r's mesh filter (its high word only exists with more than 32 meshes)
+__device__ __forceinline__ unsigned long long mask_read(unsigned long long m, uint32_t r, int meshes) {
+  const uint32_t lo = lane_read((uint32_t)m, r);
+  return meshes > 32 ? ((unsigned long long)lane_read((uint32_t)(m >> 32), r) << 32) | lo : lo;
+}
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
@@ -737,7 +750,7 @@ __device__ __forceinline__ float wave_max_all(float v) {
 __device__ __forceinline__ Bundle make_bundle(bool sel, f3 d) {
   const int lead = __builtin_ctzll(__ballot(sel));
   Bundle b;
-  b.a = mk(__shfl(d.x, lead, 64), __shfl(d.y, lead, 64), __shfl(d.z, lead, 64));
+  b.a = mk(lane_read(d.x, (uint32_t)lead), lane_read(d.y, (uint32_t)lead), lane_read(d.z, (uint32_t)lead));
   const float lam = sel ? dot(d, b.a) : 3.0f;
   b.c_lo = wave_min_all(lam) - 1e-5f;
   b.c_hi = 1.00001f;
@@ -944,7 +957,7 @@ __device__ __forceinline__ uint32_t world_hit_tile(const Scene& sc, const TraceP
   const bool octant = tl.aabb_ok && fabsf(d.x) <= 1.5f && fabsf(d.y) <= 1.5f && fabsf(d.z) <= 1.5f;
   const uint32_t oct = (fbits(d.x) >> 31) | ((fbits(d.y) >> 31) << 1) | ((fbits(d.z) >> 31) << 2);
   unsigned long long pm = tl.aabb >> oct;
-  const uint32_t oct_tests = (uint32_t)__shfl((int)tl.tsum, (int)oct, 64);
+  const uint32_t oct_tests = lane_read(tl.tsum, oct);
   if (prim && octant) {
     tests += oct_tests;
   } else if (prim) {
@@ -1496,12 +1509,15 @@ struct WqLds {
 };
 
 __device__ __forceinline__ f3 shfl3(f3 v, uint32_t r) {
-  return mk(__shfl(v.x, (int)r, 64), __shfl(v.y, (int)r, 64), __shfl(v.z, (int)r, 64));
+  return mk(lane_read(v.x, r), lane_read(v.y, r), lane_read(v.z, r));
 }
 
 // BUNDLE_WQ node image (hrt_bvh.h make_wq_nodes): 3 float4 per node, cone in binary16.
 __device__ __forceinline__ float half_lo(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xFFFFu)); }
 __device__ __forceinline__ float half_hi(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); }
+// The cone's sine from its image word: the image holds S >= sin^2 x 1.00001 (hrt_bvh.h [10]), so
+// sqrt(S), widened by the hardware root's error, is an upper bound of sin
+__device__ __forceinline__ float wq_sin_up(uint32_t w10) { return __builtin_amdgcn_sqrtf(half_lo(w10)) * 1.0000005f; }
 __device__ __forceinline__ uint32_t wq_info(const float4* nodes, uint32_t k) {  // leaf info / right child
   return __builtin_bit_cast(uint32_t, nodes[3 * k + 2].w);
 }
@@ -1530,7 +1546,7 @@ __device__ __forceinline__ bool wq_node_visit_r(const float4& N0, const float4& 
   const float x = half_lo(w8) * d.x + half_hi(w8) * d.y + half_lo(w9) * d.z;
   const float xa = fmaxf(fabsf(x) - (2e-6f + kWqAxisErr), 0.0f);
   const float s_up = __builtin_amdgcn_sqrtf(fmaxf(1.0f - xa * xa, 0.0f)) + 1.2e-6f;
-  if (HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f) return false;  // back
+  if (HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * wq_sin_up(w10) - 1e-6f > 1e-5f) return false;  // back
   const float mg = N0.w + N1.w * R;
   const float tx0 = ((N0.x - mg) - o.x) * inv.x, tx1 = ((N1.x + mg) - o.x) * inv.x;
   const float ty0 = ((N0.y - mg) - o.y) * inv.y, ty1 = ((N1.y + mg) - o.y) * inv.y;
@@ -1586,16 +1602,17 @@ __device__ __forceinline__ bool wq_member_visit(const float4& N0, const float4& 
   // The test below squared, without the square root and only ever stricter.  It is back <=> L > s_up sin
   // with L = (x - E) cos - 1.1e-5 and s_up = sqrt(q) + 1.2e-6 (q = max(1 - xa^2, 0); the hardware root is
   // within 1.2e-7 of sqrt(q) on [0, 1]).  Here: L' = (x - E) cos - 1.2e-5 (its two roundings < 2.4e-7
-  // below the 1e-6 extra), and s_up^2 <= (sqrt(q) + 1.4e-6)^2 <= q + 3e-6 (sqrt(q) <= 1); the four
-  // roundings of the right-hand side (< 2.4e-7 relative) inside the x1.00001.  L' > 0 and L'^2 > that
-  // imply L > s_up sin.  NaN -> not back.
+  // below the 1e-6 extra), and s_up^2 <= (sqrt(q) + 1.4e-6)^2 <= q + 3e-6 (sqrt(q) <= 1); the image's
+  // S >= sin^2 x 1.00001 (rounded up, hrt_bvh.h [10]) leaves the two roundings of (q2 + 3e-6) S and the one
+  // of L'^2 (< 1.8e-7 relative) far inside the x1.00001.  L' > 0 and L'^2 > that imply L > s_up sin.
+  // (r04: S precomputed -- one mixed-precision multiply instead of a conversion and three multiplies)
+  // NaN -> not back.
   const float q2 = fmaxf(__builtin_fmaf(-xa, xa, 1.0f), 0.0f);
-  const float sn = half_lo(w10);
   const float L = __builtin_fmaf(x - kWqAxisErr, half_hi(w9), -1.2e-5f);
-  const bool back = HRT_WQ_CONE && L > 0.0f && L * L > ((q2 + 3e-6f) * (sn * sn)) * 1.00001f;
+  const bool back = HRT_WQ_CONE && L > 0.0f && L * L > __builtin_fmaf(q2 + 3e-6f, half_lo(w10), 0.0f);
 #else
   const float s_up = __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-xa, xa, 1.0f), 0.0f)) + 1.2e-6f;
-  const bool back = HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * half_lo(w10) - 1e-6f > 1e-5f;
+  const bool back = HRT_WQ_CONE && (x - kWqAxisErr) * half_hi(w9) - s_up * wq_sin_up(w10) - 1e-6f > 1e-5f;
 #endif
 #if !HRT_WQ_BRANCHLESS
   if (back) return false;
@@ -1730,11 +1747,11 @@ struct BandFlat {
     const uint32_t v = lds_get(&marks[lane]);
     const unsigned long long m = __ballot(v != 0u) & (lane == 63u ? ~0ull : (2ull << lane) - 1ull);
     const uint32_t s = m ? 63u - (uint32_t)__builtin_clzll(m) : 0u;
-    const uint32_t sv = (uint32_t)__shfl((int)v, (int)s, 64);
+    const uint32_t sv = lane_read(v, s);
     own = m ? sv - 1u : carry;
     carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
     const uint32_t gi = base + lane;
-    const uint32_t k = (uint32_t)__shfl((int)delta, (int)own, 64) + gi;
+    const uint32_t k = lane_read(delta, own) + gi;
     return gi < total ? k : 0u;
   }
 };
@@ -1787,9 +1804,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     tc -= 64u;
     wave_handoff();
     const uint32_t e = lds_get(&wq.ts[tc + lane]), r = e & 63u;
-    const unsigned long long rm =
-        ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
-        (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
+    const unsigned long long rm = mask_read(mask, r, K->pc.num_meshes);
     wq_leaf_prim(prims, wq, e >> 6, r, rm, shfl3(o, r), shfl3(d, r));
     wave_handoff();  // these pops before the round's pushes into their words
     tri_pairs += 64u;
@@ -1855,7 +1870,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       oc.d = shfl3(bc.d, own);
 #if HRT_WQ_BAND_PLANE
       const f3 oo = shfl3(o, own);
-      const float ot = __shfl(ptol, (int)own, 64);
+      const float ot = lane_read(ptol, own);
       const float sp = __builtin_fmaf(oo.z, nh.z, __builtin_fmaf(oo.y, nh.y, oo.x * nh.x)) - nh.w;
       const bool push = base + lane < total && oc.in(nh) && !(sp < -ot);
 #else
@@ -1914,9 +1929,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const uint32_t e = is_node ? lds_get(&wq.ns[nc + lane]) : is_tri ? lds_get(&wq.ts[tc + lane - nn]) : lane;
     const uint32_t r = e & 63u;
     const f3 ro = shfl3(o, r), rd = shfl3(d, r);
-    const unsigned long long rm =
-        ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(mask >> 32), (int)r, 64) << 32) |
-        (uint32_t)__shfl((int)(uint32_t)mask, (int)r, 64);
+    const unsigned long long rm = mask_read(mask, r, K->pc.num_meshes);
     if (is_tri) wq_leaf_prim(prims, wq, e >> 6, r, rm, ro, rd);
     if (nn == 0u) continue;
     // node pairs (ray r, group fc .. fc + cnt - 1): test every member.  Slot k: member k's push entry
@@ -1925,7 +1938,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     // (r03, measured slower: fetching the mesh filter only for steps with triangle pairs and abs_t as
     // abs_coef * R instead of a shuffle -- island 2.271 -> 2.276, cave 7.248 -> 7.310 ms)
     const f3 rinv = shfl3(inv, r);
-    const float rR = __shfl(R, (int)r, 64), rabs = __shfl(abs_t, (int)r, 64);
+    const float rR = lane_read(R, r), rabs = lane_read(abs_t, r);
     const bool overflow = nc + width * nn > wq.ncap - (HRT_WQ_PUSH_DUMP ? 1u : 0u);  // wave-uniform
     const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs);
     uint32_t pe[kWqSlots], li[kWqSlots];

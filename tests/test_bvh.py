@@ -254,7 +254,7 @@ def test_wq_node_image(scene):
     """BUNDLE_WQ's 48 B node image (hrt_bvh.h make_wq_nodes) with 2-member groups (the binary tree)
     against the full preorder nodes: the same boxes and margins in sibling-adjacent order (an inner
     node's children at fc, fc + 1, group word fc | 1 << 16), leaf info copied, escapes that continue a
-    stackless walk after each subtree; the binary16 cone only ever widens (cos rounded down, sin up)
+    stackless walk after each subtree; the binary16 cone only ever widens (cos rounded down, sin^2 x 1.00001 up)
     and the axis is within 2^-12 per component (kernel: 5e-4)."""
     case = SceneCase(scene, (8, 8), 1, 1)
     b = build(case.tris, case.meshes, 4)
@@ -293,7 +293,9 @@ def test_wq_node_image(scene):
     axis = N[:, 8:11].astype(np.float64)
     assert np.abs(np.stack([ax, ay, az], 1) - axis).max() <= 2.0 ** -12
     assert (cq <= N[:, 11].astype(np.float64)).all() and (cq >= 0).all()
-    assert (sq >= N[:, 12].astype(np.float64)).all()
+    sin = N[:, 12].astype(np.float64)
+    assert (sin >= 0).all() and (sq >= sin * sin * 1.00001).all()  # S >= sin^2 x 1.00001, rounded up
+    assert (sq <= sin * sin * 1.00001 * (1 + 2.0 ** -10) + 2.0 ** -24).all()  # and within 1 ulp (subnormals: 2^-24)
     assert np.linalg.norm(np.stack([ax, ay, az], 1) - axis, axis=1).max() <= 5e-4  # |d.(A16 - A)| <= |A16 - A|
     # a stackless walk over the image visits every node once, in preorder of the full tree
     order, cur = [], 0
