@@ -1171,14 +1171,14 @@ extern "C" hrt_status hrt_debug_math_check(int device, uint32_t n, uint32_t seed
 
 // Test support: the RNG-domain shortcuts (sqrt_rng, spec_sincos_angle) against the general routines
 // over all 2^32 u01 states; out = {sqrt mismatches, sincos mismatches}.
-extern "C" hrt_status hrt_debug_math_check_rng(int device, uint64_t out[3]) {
+extern "C" hrt_status hrt_debug_math_check_rng(int device, uint64_t out[5]) {
   if (!out) return fail(nullptr, HRT_ERR_INVALID_ARGUMENT, "hrt_debug_math_check_rng: null out");
   unsigned long long* d = nullptr;
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipMalloc((void**)&d, 3 * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMemset(d, 0, 3 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc((void**)&d, 5 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(d, 0, 5 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hrt::launch_math_check_rng(d, nullptr);
-  if (e == hipSuccess) e = hipMemcpy(out, d, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(out, d, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
   if (d) (void)hipFree(d);
   if (e != hipSuccess) return hip_fail(nullptr, e, "hrt_debug_math_check_rng");
   return HRT_OK;

@@ -2930,13 +2930,20 @@ __global__ __launch_bounds__(256) void math_check_rng(uint32_t base, unsigned lo
   const bool bad_fast = rho_nz != (u != 0.0f && u != 1.0f) || c3 == 0.0f ||
                         (k - 1u < 0xFFFFFF7Fu) != (u != 0.0f && u != 1.0f);  // adjust_dir's HRT_FUZZ_INT test
   const bool bad_log = fbits(spec_log_u01(u)) != fbits(spec_log(u));
+  // the folded u01 scalings of get_ray_dir and normal_dist (u01_mul), exact by construction
+  const bool bad_mul = fbits(u01_mul(k, 3.14159265358979323846f * 0x1p-31f)) != fbits(r) ||
+                       fbits(u01_mul(k, 6.2831852f * 0x1p-32f)) != fbits(th);
   if (bad_sqrt) atomicAdd(&out[0], 1ull);
+  // the hardware square root alone against the correctly rounded one on both domains (out[3], out[4]):
+  // where it never differs, sqrt_rng needs no correction steps
+  if (fbits(__builtin_amdgcn_sqrtf(u)) != fbits(__builtin_sqrtf(u))) atomicAdd(&out[3], 1ull);
+  if (fbits(__builtin_amdgcn_sqrtf(l)) != fbits(__builtin_sqrtf(l))) atomicAdd(&out[4], 1ull);
   if (bad_sc) atomicAdd(&out[1], 1ull);
   // rcp_core(b) = RN(1/b) for every float b in [2^-40, 2^40] (k read as a float), the premise of
   // div_core's one correction
   const float bk = bitsf(k);
   const bool bad_rcp = bk >= 0x1p-40f && bk <= 0x1p40f && fbits(rcp_core(bk)) != fbits(1.0f / bk);
-  if (bad_fast || bad_log || bad_rcp) atomicAdd(&out[2], 1ull);
+  if (bad_fast || bad_log || bad_rcp || bad_mul) atomicAdd(&out[2], 1ull);
 }
 // hrt_debug_band_flatten: BandFlat on 64 given lists (n[l], b0[l]); out[(r * 64 + l) * 2 + {0, 1}] = the
 // owner and entry of slot r * 64 + l for each round r < rounds, and out[rounds * 128] = total.

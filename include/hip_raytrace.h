@@ -451,8 +451,10 @@ hrt_status hrt_debug_unmap_memory(void* ptr, uint64_t size);
 hrt_status hrt_debug_math_check(int device, uint32_t n, uint32_t seed, uint64_t out[4]);
 /* Test support: the kernels' RNG-domain shortcuts (sqrt of u01 draws and of -2 log(u01), sin/cos of the
  * RNG's angles without the range guard) against the general routines over all 2^32 states.
- * out = {sqrt mismatches, sincos mismatches, Lambertian-shortcut premise violations (hrt_kernels.hip adjust_dir)}. */
-hrt_status hrt_debug_math_check_rng(int device, uint64_t out[3]);
+ * out = {sqrt mismatches, sincos mismatches, Lambertian-shortcut premise or folded-scaling violations
+ * (hrt_kernels.hip adjust_dir, hrt_math.h u01_mul), values where the bare hardware square root differs from
+ * the correctly rounded one on u01 draws, and on -2 log(u01)}. */
+hrt_status hrt_debug_math_check_rng(int device, uint64_t out[5]);
 /* Test support: the trace kernel's flattening of a wave's grazing-band lists (64 lanes, lane l's list
  * of n[l] entries starting at entry b0[l]) into 64-slot rounds.  owner_entry[(r * 64 + l) * 2 + {0, 1}] =
  * the owner lane and entry index of slot r * 64 + l (entry 0 past the end), r < rounds <= 4096;
