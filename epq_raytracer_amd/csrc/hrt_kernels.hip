@@ -1097,6 +1097,7 @@ struct Coop {
   // low-spp frames -- 4K 4 spp took 5.1 ms per frame)
   bool defer = false;
   unsigned long long acc_s = 0, acc_t = 0, acc_m = 0;
+  bool hot = false;              // the item's wave runs at issue priority 3 (tile_loop)
 };
 
 __device__ __forceinline__ void coop_merge(Coop& co, Closest& c) {
@@ -2183,6 +2184,14 @@ __device__ __forceinline__ void sky_samples(const TileList& tl, bool active, f3 
   }
 }
 
+// Issue priorities (s_setprio): heavy items' waves run at 3 (tile_loop), a light item's wave at 0 and
+// at HRT_BOUNCE_PRIO during its bounce traversals -- the dependent LDS / L2 chains go first and the
+// other waves' ALU work fills in behind them (r04z: cave 5.508 -> 5.433 ms per frame, island unchanged;
+// light items at 1 or 2 with sky waves at 0, or bounce priority 2 or 3, no better;
+// profiles/r04/r04z*_ab_*.jsonl)
+#ifndef HRT_BOUNCE_PRIO
+#define HRT_BOUNCE_PRIO 1
+#endif
 // kBounceWqR: BUNDLE_WQ with node margins from each member's own R (HRT_OPT_WQ_NODE_RADIUS = 2)
 enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2, kBounceWq = 3, kBounceWqR = 4 };
 constexpr bool is_wq(int b) { return b == kBounceWq || b == kBounceWqR; }
@@ -2300,6 +2309,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     }
     if (D && P.diag) t1 = __builtin_readcyclecounter();
     if (run_sec) {
+      if (HRT_BOUNCE_PRIO && !co.hot) __builtin_amdgcn_s_setprio(HRT_BOUNCE_PRIO);
       if constexpr (is_wq(Bounce)) {
         world_hit_bounce_wq<D, Bounce == kBounceWqR>(HRT_SHADE_KARGS ? kscene() : sc, P, bsrc, sec, p.pos, p.dir, tests,
                                                      c, dg);
@@ -2311,6 +2321,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
         if (sec) c = world_hit_brute(sc, src, pc, p.pos, p.dir, tests);
       }
     }
+    if (HRT_BOUNCE_PRIO && run_sec && !co.hot) __builtin_amdgcn_s_setprio(0);
     if (D && P.diag) t2 = __builtin_readcyclecounter();
     if (prim || sec) {
       ++segs;
@@ -2569,6 +2580,7 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     if (lane >= (64u >> lk)) x = 0xFFFFFFFFu;  // idle lane of a split item
     const uint64_t t0 = __builtin_readcyclecounter();
     if (hot) __builtin_amdgcn_s_setprio(3);
+    solo.hot = hot;
     solo.work = 0;
     body(x, lr, solo, tf, run);
     if (hot) __builtin_amdgcn_s_setprio(0);
