@@ -2529,7 +2529,7 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
 #endif
   constexpr uint32_t kGrab = HRT_GRAB;
 #ifndef HRT_GRAB_TAIL
-#define HRT_GRAB_TAIL 24u  // items per resident wave taken singly at the end (r04ad: 64 -> 24, island 1.804 -> 1.782, cave 5.434 -> 5.406 ms)
+#define HRT_GRAB_TAIL 64u  // items per resident wave taken singly at the end (16 x the r01s grab of 4)
 #endif
   const uint32_t resident = gridDim.x * (BLOCK / 64);
   uint32_t cur = first, end = first;
