@@ -25,14 +25,9 @@
 #include "hrt_host.h"
 #include "hrt_kernels.h"
 
-static_assert(sizeof(hrt_material) == 48, "std430 RayTracingMaterial");
-static_assert(sizeof(hrt_ray) == 16, "std430 Ray");
-static_assert(sizeof(hrt_sphere) == 64, "std430 Sphere");
-static_assert(sizeof(hrt_triangle) == 64, "std430 Triangle");
-static_assert(sizeof(hrt_mesh) == 80, "std430 Mesh");
-static_assert(sizeof(hrt_push_constants) == 124, "push constant block (src/raytrace_pipeline.rs:125-139)");
-static_assert(offsetof(hrt_push_constants, num_rays) == 80, "push layout");
-static_assert(offsetof(hrt_push_constants, height) == 120, "push layout");
+// (the record, push-block, hrt_create_info / hrt_layout / hrt_stats sizes and offsets are
+// static_asserted by include/hip_raytrace.h itself, for every translation unit that includes it)
+static_assert(sizeof(hrt_stats) == 64, "hrt_stats: ABI 4");
 
 namespace {
 
@@ -1184,8 +1179,8 @@ extern "C" hrt_status hrt_debug_math_check_rng(int device, uint64_t out[5]) {
   return HRT_OK;
 }
 
-// Test support: the band lists' wave flattening (hrt_kernels.hip BandFlat) on 64 given lists;
-// owner_entry[(r * 64 + l) * 2 + {0, 1}] = owner lane and entry of slot r * 64 + l, r < rounds.
+// Test support: the pair traversal's cross-lane LDS handoffs (hrt_kernels.hip lds_put / lds_get /
+// wq_slot_*, wave_handoff) on a scripted run of one wave; the host model is tests/test_gpu_boundary.py's.
 extern "C" hrt_status hrt_debug_wq_protocol(int device, uint32_t rounds, const uint32_t* cnt, const uint32_t* take,
                                             const uint32_t* tgt, const uint64_t* val, const uint64_t seed[64],
                                             uint32_t* popped, uint64_t* seen, uint64_t slots[64], uint32_t* depth) {
@@ -1225,6 +1220,8 @@ extern "C" hrt_status hrt_debug_wq_protocol(int device, uint32_t rounds, const u
   return HRT_OK;
 }
 
+// Test support: the band lists' wave flattening (hrt_kernels.hip BandFlat) on 64 given lists;
+// owner_entry[(r * 64 + l) * 2 + {0, 1}] = owner lane and entry of slot r * 64 + l, r < rounds.
 extern "C" hrt_status hrt_debug_band_flatten(int device, const uint32_t n[64], const uint32_t b0[64], uint32_t rounds,
                                              uint32_t* owner_entry, uint32_t* total) {
   if (!n || !b0 || !owner_entry || !total || rounds == 0 || rounds > 4096)

@@ -135,9 +135,9 @@ struct hrt_context {
   uint32_t bvh_leaf = 0;  // HRT_OPT_BVH_LEAF_SIZE for the next hrt_set_scene (0 = auto, hrt_bvh.h)
   uint32_t wq_node_radius = 0;  // HRT_OPT_WQ_NODE_RADIUS (0 = auto)
   uint32_t bvh_width = 4;  // HRT_OPT_BVH_WIDTH (hrt_bvh.h kWqDefaultWidth) for the next hrt_set_scene
-  int64_t debug_fail_alloc = 0;
+  int64_t debug_fail_alloc = 0;   // debug build: fail the n-th device allocation of the next hrt_set_scene
   uint32_t debug_grab_runs = 0;   // debug build: HRT_DEBUG_OPT_GRAB_RUNS
-  uint32_t debug_wq_tri_cap = 0;  // debug build: HRT_DEBUG_OPT_WQ_TRI_CAP  // debug build: fail the n-th device allocation of the next hrt_set_scene
+  uint32_t debug_wq_tri_cap = 0;  // debug build: HRT_DEBUG_OPT_WQ_TRI_CAP (triangle-pair stack capacity)
 
   int variant = 0;
   bool counters_on = true;

@@ -88,11 +88,20 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long b) {
 // a Hillis-Steele scan inside each row of 16 lanes by DPP row shifts (lanes past a row's start read 0),
 // then each row adds the totals of the rows before it by the row broadcasts of lanes 15 and 31 -- six
 // adds with DPP operands instead of a ballot, two lane counts and a shift per bit of x.
+// The DPP form is GFX9 wave64 only (row_bcast:15/31 do not exist on GFX10+) and needs every lane active
+// (an inactive lane's row sum would be missing from the broadcast): other targets take the ballot scan,
+// and HRT_KERNEL_ASSERTS=1 builds check the exec mask on entry.
 #ifndef HRT_DPP_SCAN
 #define HRT_DPP_SCAN 1
 #endif
+#ifndef HRT_KERNEL_ASSERTS
+#define HRT_KERNEL_ASSERTS 0
+#endif
 __device__ __forceinline__ uint32_t wave_scan_excl(uint32_t x, uint32_t& total, uint32_t bits = 32u) {
-#if HRT_DPP_SCAN
+#if HRT_KERNEL_ASSERTS
+  if (__builtin_amdgcn_read_exec() != ~0ull) __builtin_trap();
+#endif
+#if HRT_DPP_SCAN && (defined(__GFX9__) || !defined(__HIP_DEVICE_COMPILE__))
   (void)bits;
   // (inline: hipcc left each __builtin_amdgcn_mov_dpp as a separate move before a plain add.  Each step
   // reads the previous one's result through DPP, which needs two wait states after a VALU write: the
@@ -2251,7 +2260,8 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   }
   while (__any(!done)) {
     if (!done && p.bounce > pc.max_bounces) {
-      if (sample >= pc.num_samples && fr + 1u < nrun) {  // the pixel's next frame of the run
+      // (a while: with num_samples <= 0 every frame of the run ends at once and each must still be stored)
+      while (sample >= pc.num_samples && fr + 1u < nrun) {  // the pixel's next frame of the run
         store_pixel(P, x, lr, div3(colour, (float)pc.num_samples), frame + fr);
         ++fr;
         colour = mk(0.0f, 0.0f, 0.0f);

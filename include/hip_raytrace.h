@@ -159,14 +159,40 @@ typedef struct hrt_stats {
   uint64_t accumulates;   /* combiner dispatches since reset */
   float last_trace_ms;    /* device time of the last trace dispatch (HIP events) */
   float total_trace_ms;   /* device time of all trace dispatches since reset */
-  uint64_t wave_steps;    /* sum over waves of the wave's longest per-lane segment count: lane
-                             efficiency = segments / (64 * wave_steps) */
+  uint64_t wave_steps;    /* sum over work items of the item's longest per-lane segment count: lane
+                             efficiency = segments / (64 * wave_steps).  A frame run of a multi-frame
+                             launch (hrt_compute_n) is one item: its lanes' segments summed over the run's
+                             frames, so the figure is comparable between launches of the same shape only */
   uint32_t last_kernel;   /* hrt_kernel the last trace ran (HRT_KERNEL_AUTO resolved) */
   uint32_t last_block;    /* its workgroup size (threads) */
   uint32_t last_frames;   /* frames the last trace launch held (hrt_compute_n packs up to
                              HRT_OPT_FRAMES_PER_LAUNCH into one launch; 1 for hrt_trace) (ABI 4) */
   uint32_t reserved;
 } hrt_stats;
+
+/* The layouts every binding relies on (the Rust declarations in INTEGRATION.md are checked against
+ * these by tests/test_rust_binding.py): std430 record sizes, the push block, and the host structs. */
+#ifdef __cplusplus
+#define HRT_STATIC_ASSERT(c, m) static_assert(c, m)
+#else
+#define HRT_STATIC_ASSERT(c, m) _Static_assert(c, m)
+#endif
+HRT_STATIC_ASSERT(sizeof(hrt_material) == 48, "std430 RayTracingMaterial");
+HRT_STATIC_ASSERT(sizeof(hrt_ray) == 16, "std430 Ray");
+HRT_STATIC_ASSERT(sizeof(hrt_sphere) == 64, "std430 Sphere");
+HRT_STATIC_ASSERT(sizeof(hrt_triangle) == 64, "std430 Triangle");
+HRT_STATIC_ASSERT(sizeof(hrt_mesh) == 80, "std430 Mesh");
+HRT_STATIC_ASSERT(offsetof(hrt_mesh, len) == 28 && offsetof(hrt_mesh, material) == 32, "std430 Mesh layout");
+HRT_STATIC_ASSERT(sizeof(hrt_push_constants) == 124, "push constant block (src/raytrace_pipeline.rs:125-139)");
+HRT_STATIC_ASSERT(offsetof(hrt_push_constants, num_rays) == 80 && offsetof(hrt_push_constants, jitter_size) == 96 &&
+                      offsetof(hrt_push_constants, height) == 120,
+                  "push constant layout");
+HRT_STATIC_ASSERT(sizeof(hrt_create_info) == 28 && offsetof(hrt_create_info, part_count) == 24, "hrt_create_info");
+HRT_STATIC_ASSERT(sizeof(hrt_layout) == 28 && offsetof(hrt_layout, mode) == 24, "hrt_layout");
+HRT_STATIC_ASSERT(sizeof(hrt_stats) == 64 && offsetof(hrt_stats, last_trace_ms) == 32 &&
+                      offsetof(hrt_stats, wave_steps) == 40 && offsetof(hrt_stats, last_kernel) == 48 &&
+                      offsetof(hrt_stats, last_frames) == 56,
+                  "hrt_stats: 64 bytes since ABI 4");
 
 typedef struct hrt_context hrt_context;
 

@@ -87,6 +87,11 @@ def test_record_layouts_match_std430():
     assert _lib.PushConstants.jitter_size.offset == 96
     assert _lib.PushConstants.use_environment_light.offset == 104
     assert _lib.PushConstants.height.offset == 120
+    # the host structs (include/hip_raytrace.h static_asserts the same; INTEGRATION.md's Rust binding is
+    # pinned to the header by tests/test_rust_binding.py)
+    assert ctypes.sizeof(_lib.Stats) == 64
+    assert _lib.Stats.last_frames.offset == 56 and _lib.Stats.wave_steps.offset == 40
+    assert ctypes.sizeof(_lib.CreateInfo) == 28 and ctypes.sizeof(_lib.Layout) == 28
 
 
 def test_create_fails_loudly():

@@ -851,17 +851,27 @@ def test_sky_items_bit_exact(what, variant):
     ctx.close()
 
 
-@pytest.mark.parametrize("scene,variant", [("island", 9), ("cave", 9), ("island", 7), ("island", 8), ("box", 7)])
-def test_frame_runs_match_frame_loop(scene, variant):
+@pytest.mark.parametrize("scene,variant,spp", [("island", 9, 3), ("cave", 9, 3), ("island", 7, 3), ("island", 8, 3),
+                                               ("box", 7, 3), ("island", 9, 0), ("box", 7, 0), ("box", 9, -2)])
+def test_frame_runs_match_frame_loop(scene, variant, spp):
     """Frame runs (a persistent wave's grabbed items that are one tile's consecutive frames run as one
     pass: each lane starts its pixel's next frame as soon as it finishes one) give the per-frame loop's
     accumulator, last trace image and counters.  The debug library's HRT_DEBUG_OPT_GRAB_RUNS makes the
-    waves take 4 items per grab at this size (the product does so while many items remain)."""
-    case = SceneCase(scene, (75, 41), 3, 8)
+    waves take 4 items per grab at this size (the product does so while many items remain).  spp <= 0
+    (ADVICE r04): every frame of a run ends at once and each must still be stored.  wave_steps is not
+    compared: inside a run it is the largest per-lane segment sum over the run, not a sum of per-frame
+    maxima (hrt_stats.wave_steps)."""
+    case = SceneCase(scene, (75, 41), spp, 8)
+
+    def push(k):
+        pc = case.push(k)
+        pc.num_samples = spp  # (SceneCase clamps to >= 1)
+        return pc
+
     first, n = 5, 11
     loop = case.context(variant=variant)
     for k in range(first, first + n):
-        loop.trace(case.push(k))
+        loop.trace(push(k))
         loop.accumulate(k)
     a = loop.stats()
     want_acc, want_trace = loop.read(_lib.IMG_ACCUM), loop.read(_lib.IMG_TRACE)
@@ -871,7 +881,7 @@ def test_frame_runs_match_frame_loop(scene, variant):
         ctx = case.context(variant=variant, debug=True,
                            options={_lib.OPT_FRAMES_PER_LAUNCH: 16, _lib.DEBUG_OPT_GRAB_RUNS: grab,
                                     _lib.OPT_BVH_LEAF_SIZE: 4 if variant == 8 else 0})
-        ctx.compute_n(case.push(first), n)
+        ctx.compute_n(push(first), n)
         b = ctx.stats()
         got_acc, got_trace = ctx.read(_lib.IMG_ACCUM), ctx.read(_lib.IMG_TRACE)
         ctx.close()
