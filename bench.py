@@ -446,6 +446,16 @@ def pmc_roofline(args, world, kernel_sym, kern_ms, tests_per_frame, row_frac, la
                                                                   if world > 1 else "")))
     out["traffic"] = round(traffic) if traffic else None
     out["valu_issue_utilisation"] = pmc.get("valu_issue_utilisation")
+    # lane-weighted: the FP32 FLOPs the ACTIVE lanes execute (executed x the VALU lane utilisation,
+    # SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU) of the same record); frac above counts every
+    # wave-instruction as 64 lanes whatever the exec mask
+    lane_util = pmc.get("valu_lane_utilisation")
+    if flops and lane_util:
+        lane_tf = flops * lane_util / (kern_ms * 1e-3) / 1e12
+        out.update(lane_flops=round(lane_tf, 3), lane_frac=round(lane_tf / FP32_PEAK_TFLOPS, 4),
+                   live_lane_ratio=round(lane_util, 4))
+    else:
+        out.update(lane_flops=None, lane_frac=None, live_lane_ratio=None)
     out["pmc_source"] = os.path.relpath(args.pmc_json, ROOT)
     return out
 

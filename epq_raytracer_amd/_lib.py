@@ -67,7 +67,7 @@ class Stats(ctypes.Structure):
                 ("reserved", c_uint32)]
 
 
-ABI_VERSION = 4  # HRT_ABI_VERSION this binding's signatures describe
+ABI_VERSION = 5  # HRT_ABI_VERSION this binding's signatures describe
 HRT_OK = 0
 STATUS_NAMES = {0: "HRT_OK", 1: "HRT_ERR_INVALID_ARGUMENT", 2: "HRT_ERR_NO_DEVICE", 3: "HRT_ERR_OUT_OF_MEMORY",
                 4: "HRT_ERR_NO_SCENE", 5: "HRT_ERR_HIP", 6: "HRT_ERR_IO", 7: "HRT_ERR_COMM"}
@@ -83,6 +83,7 @@ OPT_COMM_TIMEOUT_MS, OPT_DEFER_COMBINE = 17, 18
 DEBUG_OPT_FAIL_ALLOC = 1001  # libhip_raytrace_debug.so only
 DEBUG_OPT_WQ_TRI_CAP = 1002  # libhip_raytrace_debug.so only
 DEBUG_OPT_GRAB_RUNS = 1003  # libhip_raytrace_debug.so only
+DEBUG_OPT_TIMELINE = 1004  # builds with -DHRT_TIMELINE=1 only (tools/timeline.py)
 COMM_ID_BYTES = 128
 COMM_NONE, COMM_RCCL, COMM_RCCL_GROUP, COMM_DEVICE_COPY = 0, 1, 2, 3
 # hrt_kernel (include/hip_raytrace.h)
@@ -116,7 +117,8 @@ DIAG_NAMES = ("primary_iters", "primary_considered", "primary_survivors", "bounc
               "bounce_survivors", "bounce_lanes", "bvh_visits", "bvh_prim_tests", "bvh_band_tests", "primary_cycles", "bounce_cycles",
               "shade_cycles", "bounce_stage2", "bounce_front", "bvh_trips",
               "bvh_leaf_trips", "band_scan_max", "band_scan_len", "sky_items", "sky_cycles",
-              "primary_lanes", "loop_iters", "live_lanes")
+              "primary_lanes", "loop_iters", "live_lanes", "wq_steps_16", "wq_steps_32", "wq_steps_48",
+              "wq_steps_64", "wq_members")
 SCENE_INFO_NAMES = ("bvh_nodes", "bvh_prims", "bvh_irregular", "bvh_never", "bvh_built", "bvh_band_entries",
                     "bvh_sah_milli", "bvh_margin_milli")
 
@@ -126,6 +128,7 @@ EXPORTED_SYMBOLS = (
     "hrt_read_image", "hrt_load_accumulator", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
     "hrt_get_diagnostics", "hrt_get_tile_profile", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
     "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory", "hrt_debug_math_check", "hrt_debug_math_check_rng", "hrt_debug_band_flatten", "hrt_debug_wq_protocol",
+    "hrt_debug_timeline",
     "hrt_stream", "hrt_last_error", "hrt_comm_unique_id", "hrt_comm_init", "hrt_comm_init_all", "hrt_comm_info",
     "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
     "hrt_debug_bvh_build", "hrt_debug_bvh_wq_nodes",
@@ -196,6 +199,7 @@ def load(debug: bool = False) -> ctypes.CDLL:
         "hrt_debug_math_check_rng": (c_int32, [c_int32, P]),
         "hrt_debug_band_flatten": (c_int32, [c_int32, P, P, c_uint32, P, P]),
         "hrt_debug_wq_protocol": (c_int32, [c_int32, c_uint32, P, P, P, P, P, P, P, P, P]),
+        "hrt_debug_timeline": (c_int32, [c_void_p, P, c_uint32, P]),
         "hrt_debug_bvh_build": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, P, c_uint64, P, c_uint64, P,
                                           c_uint64, P, c_uint64, P, c_uint64]),
         "hrt_debug_bvh_wq_nodes": (c_int64, [P, c_uint32, P, c_uint32, c_uint32, c_uint32, P, c_uint64]),

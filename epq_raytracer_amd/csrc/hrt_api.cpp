@@ -383,6 +383,8 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
   free_dev(ctx, ctx->scratch);
   free_dev(ctx, ctx->counters);
   free_dev(ctx, ctx->tile_cycles);
+  free_dev(ctx, ctx->timeline);
+  free_dev(ctx, ctx->timeline_count);
   free_dev(ctx, ctx->frame_stack);
   free_dev(ctx, ctx->ring);
   if (ctx->fold_done) (void)hipEventDestroy(ctx->fold_done);
@@ -651,6 +653,9 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.wq_ncap = ctx->wq_node_cap;  // request; launch_trace sizes the stacks
   p.wq_tcap = ctx->debug_wq_tri_cap;  // (debug) request
   p.grab_always = ctx->debug_grab_runs;  // (debug) frame runs at any size
+  p.timeline = ctx->timeline;
+  p.timeline_count = ctx->timeline_count;
+  p.timeline_cap = ctx->timeline_cap;
   p.plan_valid = lane.plan_valid ? 1u : 0u;
   p.num_cus = ctx->grid_cus ? std::min(ctx->grid_cus, ctx->num_cus) : ctx->num_cus;
   const bool built = s.bvh_info[HRT_SCENE_BVH_BUILT] != 0;
@@ -699,6 +704,7 @@ bool builds_camera_lists(int k) {
 hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stream, int l) {
   if (ctx->diag_on)
     HRT_HIP(ctx, hipMemsetAsync(ctx->tile_cycles, 0, ctx->num_tiles() * 4 * sizeof(unsigned long long), stream));
+  if (ctx->timeline) HRT_HIP(ctx, hipMemsetAsync(ctx->timeline_count, 0, sizeof(uint32_t), stream));  // this launch's
   const int variant = ctx->variant;
   if (ctx->pending.size() >= kMaxPending) {
     hrt_status st = harvest_one(ctx);
@@ -1404,9 +1410,39 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
     case HRT_DEBUG_OPT_GRAB_RUNS:
       return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "debug option: only libhip_raytrace_debug.so accepts it");
 #endif
+    case HRT_DEBUG_OPT_TIMELINE:
+#if HRT_TIMELINE
+      if (value <= 0 || value > (1 << 24)) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "timeline capacity in [1, 2^24]");
+      if (ctx->timeline) {
+        HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        free_dev(ctx, ctx->timeline);
+        free_dev(ctx, ctx->timeline_count);
+      }
+      HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->timeline, (size_t)value * 3 * sizeof(unsigned long long)));
+      HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->timeline_count, sizeof(uint32_t)));
+      HRT_HIP(ctx, hipMemset(ctx->timeline_count, 0, sizeof(uint32_t)));
+      ctx->timeline_cap = (uint32_t)value;
+      return HRT_OK;
+#else
+      return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "timeline option: only builds with -DHRT_TIMELINE=1 accept it");
+#endif
     default:
       return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "unknown option key");
   }
+}
+
+// Test / tuning support (HRT_TIMELINE builds): the last trace launch's per-item records.
+extern "C" hrt_status hrt_debug_timeline(hrt_context* ctx, uint64_t* out, uint32_t cap, uint32_t* count) {
+  if (!ctx || !out || !count) return HRT_ERR_INVALID_ARGUMENT;
+  if (!ctx->timeline) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_debug_timeline: HRT_DEBUG_OPT_TIMELINE not set");
+  if (bind(ctx) != HRT_OK) return HRT_ERR_HIP;
+  HRT_HIP(ctx, hipDeviceSynchronize());
+  uint32_t n = 0;
+  HRT_HIP(ctx, hipMemcpy(&n, ctx->timeline_count, sizeof n, hipMemcpyDeviceToHost));
+  n = std::min(n, ctx->timeline_cap);
+  *count = n;
+  HRT_HIP(ctx, hipMemcpy(out, ctx->timeline, (size_t)std::min(n, cap) * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return HRT_OK;
 }
 
 // Work the caller enqueues on the stream follows every accumulate so far: the deferred ones are folded.

@@ -737,6 +737,8 @@ struct Diag {
   uint32_t sky_items = 0;                       // work items run by sky_samples
   uint64_t cyc_sky = 0;                         // ... and their shader clocks
   uint32_t prim_lanes = 0, loop_iters = 0, live_lanes = 0;  // fused-loop lane use
+  uint32_t wq_fill[4] = {0, 0, 0, 0};  // BUNDLE_WQ: node steps with 1-16 / 17-32 / 33-48 / 49-64 node pairs
+  uint32_t wq_members = 0;             // ... the members of the groups this lane popped (valid slots), summed
 };
 
 __device__ __forceinline__ float wave_min_all(float v) {  // all 64 lanes active
@@ -1500,6 +1502,12 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_EARLY_REC
 #define HRT_WQ_EARLY_REC 1  // a node step's first member pair read before the slot read (r04)
 #endif
+#ifndef HRT_TIMELINE
+#define HRT_TIMELINE 0  // per-item timeline records (tools/timeline.py; A/B builds only)
+#endif
+#ifndef HRT_WQ_BAND_EARLY
+#define HRT_WQ_BAND_EARLY 0  // (r05b: neutral, island 1.786 / 1.787, cave 5.405 / 5.400 ms) a bounce lane's direction-cell offsets requested at the batch's start (r05)
+#endif
 #ifndef HRT_WQ_TRI_MIN
 #define HRT_WQ_TRI_MIN 64u  // a triangle step runs once this many triangle pairs wait (or no node pair is left)
 #endif
@@ -1776,6 +1784,18 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
   const float4* prims = K->bvh_prims;
   const float rel_t = K->bvh_rel_t, abs_coef = K->bvh_abs_coef;
   const uint32_t tcap = K->wq_tcap;
+#if HRT_WQ_BAND_EARLY
+  // the lane's direction-cell offsets requested first: the band rounds' first dependent global read (a
+  // random line of a structure far larger than an XCD's L2) then overlaps the spheres, the reciprocals,
+  // the meshes' AABB tests and the irregular list instead of starting after them
+  uint32_t cb0 = 0, cb1 = 0;
+  if (sec) {
+    const uint32_t* band_off = K->bvh_band_off;
+    const uint32_t cell = dir_cell(d, K->bvh_dir_res);
+    cb0 = band_off[cell];
+    cb1 = band_off[cell + 1];
+  }
+#endif
   spheres_first(sc, pc, sec, o, d, c);
   const f3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // the meshes' AABB tests and the traversal
   unsigned long long mask = 0ull;
@@ -1842,12 +1862,19 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     const float ptol = 1e-5f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + K->bvh_band_a1);
 #endif
     uint32_t b0 = 0, n = 0;
+#if HRT_WQ_BAND_EARLY
+    if (sec && mask) {
+      b0 = cb0;
+      n = cb1 - cb0;
+    }
+#else
     if (sec && mask) {
       const uint32_t* band_off = K->bvh_band_off;
       const uint32_t cell = dir_cell(d, K->bvh_dir_res);
       b0 = band_off[cell];
       n = band_off[cell + 1] - b0;
     }
+#endif
     if (D && P.diag) {
       dg.band_len += n;
       band_lmax = n;
@@ -1934,7 +1961,9 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     nc -= nn;
     node_pairs += nn;
     tri_pairs += tn;
+    const bool overflow = nc + width * nn > wq.ncap - (HRT_WQ_PUSH_DUMP ? 1u : 0u);  // wave-uniform
     const bool is_node = lane < nn, is_tri = lane >= nn && lane < nn + tn;
+    if (D && P.diag && nn) ++dg.wq_fill[(nn - 1u) >> 4];
     wave_handoff();  // the last step's pushes and slot lowerings before this step's pops and reads
     const uint32_t e = is_node ? lds_get(&wq.ns[nc + lane]) : is_tri ? lds_get(&wq.ts[tc + lane - nn]) : lane;
     const uint32_t r = e & 63u;
@@ -1949,7 +1978,6 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     // abs_coef * R instead of a shuffle -- island 2.271 -> 2.276, cave 7.248 -> 7.310 ms)
     const f3 rinv = shfl3(inv, r);
     const float rR = lane_read(R, r), rabs = lane_read(abs_t, r);
-    const bool overflow = nc + width * nn > wq.ncap - (HRT_WQ_PUSH_DUMP ? 1u : 0u);  // wave-uniform
     const WqRay rq = wq_ray(ro, rd, rinv, rR, rabs);
     uint32_t pe[kWqSlots], li[kWqSlots];
     float pk[kWqSlots];
@@ -1961,6 +1989,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     }
     if (is_node) {
       const uint32_t g = e >> 6, fc = g & 0xFFFFu, gcnt = (g >> 16) + 1u;
+      if (D && P.diag) dg.wq_members += gcnt;
       if (!overflow) {
 #if HRT_WQ_EARLY_REC
         // the first member pair's records are requested before the slot read: that read is an atomic
@@ -2403,7 +2432,12 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     atomicAdd(&P.diag[21], (unsigned long long)dg.prim_lanes);
     atomicAdd(&P.diag[22], (unsigned long long)dg.loop_iters);
     atomicAdd(&P.diag[23], (unsigned long long)dg.live_lanes);
+    if (is_wq(Bounce)) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) atomicAdd(&P.diag[24 + b], (unsigned long long)dg.wq_fill[b]);
+    }
   }
+  if (D && P.diag && is_wq(Bounce) && dg.wq_members) atomicAdd(&P.diag[28], (unsigned long long)dg.wq_members);
   if (D && P.diag && (Bounce == kBounceBvh || is_wq(Bounce))) {
     atomicAdd(&P.diag[7], (unsigned long long)dg.bvh_visits);
     atomicAdd(&P.diag[8], (unsigned long long)dg.bvh_prims);
@@ -2589,11 +2623,29 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     uint32_t x = tx * 8 + (j & 7u), lr = ty * 8 + (j >> 3);
     if (lane >= (64u >> lk)) x = 0xFFFFFFFFu;  // idle lane of a split item
     const uint64_t t0 = __builtin_readcyclecounter();
+#if HRT_TIMELINE
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (hot) __builtin_amdgcn_s_setprio(3);
     solo.hot = hot;
     solo.work = 0;
     body(x, lr, solo, tf, run);
     if (hot) __builtin_amdgcn_s_setprio(0);
+#if HRT_TIMELINE
+    if (P.timeline && lane == 0) {  // (timeline builds only: the product kernel has no such branch)
+      const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+      const uint32_t slot = atomicAdd(P.timeline_count, 1u);
+      if (slot < P.timeline_cap) {
+        const uint32_t wave = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+        P.timeline[3 * (size_t)slot] = rt0;
+        P.timeline[3 * (size_t)slot + 1] = rt1;
+        P.timeline[3 * (size_t)slot + 2] = (unsigned long long)(tile | (lk << 22) | (sub << 25) | ((uint32_t)hot << 31)) |
+                                           ((unsigned long long)(tf & 0xFFu) << 32) |
+                                           ((unsigned long long)(run & 0xFFu) << 40) |
+                                           ((unsigned long long)(wave & 0xFFFFu) << 48);
+      }
+    }
+#endif
     // cost: the work count where the body keeps one (BUNDLE_CULL_LDS), else shader clocks / 16
     const uint64_t c = CoopOk ? (uint64_t)solo.work : (__builtin_readcyclecounter() - t0) >> 4;
     prev_cost = __builtin_amdgcn_readfirstlane(c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c);

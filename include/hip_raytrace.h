@@ -39,12 +39,13 @@
 extern "C" {
 #endif
 
-/* 4 (r04): hrt_debug_wq_protocol; hrt_stats.last_frames; HRT_DIAG_SKY_* / PRIMARY_LANES / LOOP_ITERS /
+/* 5 (r05): HRT_DIAG_WQ_STEPS_* / WQ_MEMBERS (HRT_NUM_DIAG 29), HRT_DEBUG_OPT_TIMELINE + hrt_debug_timeline.
+ * 4 (r04): hrt_debug_wq_protocol; hrt_stats.last_frames; HRT_DIAG_SKY_* / PRIMARY_LANES / LOOP_ITERS /
  * LIVE_LANES (HRT_NUM_DIAG 24).
  * 3 (r03): hrt_debug_band_flatten.
  * 2 (r03): HRT_ERR_COMM, HRT_IMG_LOCAL, HRT_OPT_COMM_TIMEOUT_MS, collective error agreement;
  * hrt_debug_bvh_wq_nodes' width parameter; HRT_NUM_DIAG / HRT_NUM_SCENE_INFO grown (r02). */
-#define HRT_ABI_VERSION 4u
+#define HRT_ABI_VERSION 5u
 
 typedef enum hrt_status {
   HRT_OK = 0,
@@ -308,7 +309,11 @@ typedef enum hrt_option {
    * items 4 at a time, so a multi-frame launch runs frame runs (an item's consecutive frames in one
    * pass, hrt_kernels.hip trace_fused_split) at any image size -- the full frames take them only while
    * many items remain.  Results do not depend on it. */
-  HRT_DEBUG_OPT_GRAB_RUNS = 1003
+  HRT_DEBUG_OPT_GRAB_RUNS = 1003,
+  /* builds with -DHRT_TIMELINE=1 only (tuning, tools/timeline.py): record, for each work item the persistent
+   * kernels execute, its start / end time (s_memrealtime, 100 MHz), item word, frame, run length and
+   * resident wave -- up to value records per launch (hrt_debug_timeline).  Other builds reject the key. */
+  HRT_DEBUG_OPT_TIMELINE = 1004
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */
@@ -337,7 +342,12 @@ typedef enum hrt_diag {
   HRT_DIAG_PRIMARY_LANES = 21,     /* fused loop: primary lanes of the iterations that ran the primary path */
   HRT_DIAG_LOOP_ITERS = 22,        /* fused-loop iterations (waves) */
   HRT_DIAG_LIVE_LANES = 23,        /* ... and their lanes not yet done, summed */
-  HRT_NUM_DIAG = 24
+  HRT_DIAG_WQ_STEPS_16 = 24,       /* BUNDLE_WQ: pair steps with 1-16 node pairs (waves) */
+  HRT_DIAG_WQ_STEPS_32 = 25,       /* ... 17-32 */
+  HRT_DIAG_WQ_STEPS_48 = 26,       /* ... 33-48 */
+  HRT_DIAG_WQ_STEPS_64 = 27,       /* ... 49-64 */
+  HRT_DIAG_WQ_MEMBERS = 28,        /* ... valid members of the popped node groups, summed (vs 4 slots each) */
+  HRT_NUM_DIAG = 29
 } hrt_diag;
 
 /* What hrt_set_scene built for BUNDLE_BVH (hrt_get_scene_info). */
@@ -497,6 +507,10 @@ hrt_status hrt_debug_band_flatten(int device, const uint32_t n[64], const uint32
 hrt_status hrt_debug_wq_protocol(int device, uint32_t rounds, const uint32_t* cnt, const uint32_t* take,
                                  const uint32_t* tgt, const uint64_t* val, const uint64_t seed[64], uint32_t* popped,
                                  uint64_t* seen, uint64_t slots[64], uint32_t* depth);
+/* HRT_TIMELINE builds: the last trace launch's item records (3 words each: start, end, item | frame << 32 |
+ * run << 40 | wave << 48), at most cap of them copied; *count = the records the launch wrote (<= the
+ * HRT_DEBUG_OPT_TIMELINE capacity).  Other builds: HRT_ERR_INVALID_ARGUMENT. */
+hrt_status hrt_debug_timeline(hrt_context* ctx, uint64_t* out, uint32_t cap, uint32_t* count);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 
 /* The context's HIP stream (hipStream_t), for callers that interoperate: work enqueued on it after

@@ -1,13 +1,14 @@
 #!/bin/bash
-# r04 final GPU session for a build: GPU suite + smoke, PMC passes + bench line + rocprof kernel trace of
+# Final GPU session for a build: GPU suite + smoke, PMC passes + bench line + rocprof kernel trace of
 # the driver's shape (tools/gpu_round.sh), the cave line with its own PMC record, the self-spawned 2-rank
 # gloo rehearsal (the N > 1 line's "ranks" object), and the BASELINE configs' per-frame times.
-# Usage (via gpurun): bash tools/r04_final.sh <tag>
+# Usage (via gpurun): bash tools/final_session.sh <tag>
 set -o pipefail
-TAG=${1:-r04f}
+TAG=${1:?usage: final_session.sh <tag>}
+ROUND=${ROUND:-${TAG:0:3}}  # profiles/<round>/
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 bash tools/gpu_round.sh $TAG || exit 1
-PMC=profiles/r04/${TAG}_cave_pmc; mkdir -p $PMC
+PMC=profiles/$ROUND/${TAG}_cave_pmc; mkdir -p $PMC
 bash tools/pmc.sh $TAG/cave_pmc --scene cave > $OUT/cave_pmc.log 2>&1 || { echo "cave pmc failed"; tail -20 $OUT/cave_pmc.log; exit 1; }
 cp $OUT/cave_pmc/pmc_traffic.json $PMC/pmc_traffic.json
 timeout -k 10 600 python3 bench.py --scene cave --pmc-json $PMC/pmc_traffic.json > $OUT/bench_cave.json 2> $OUT/bench_cave.err || { echo "cave bench failed"; tail -20 $OUT/bench_cave.err; exit 1; }

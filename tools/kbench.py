@@ -106,6 +106,12 @@ def main():
                 d["live_lane_use"] = d.get("live_lanes", 0) / max(64 * d.get("loop_iters", 0), 1)
                 d["band_max_per_batch"] = d.get("band_scan_max", 0) / max(d["bounce_iters"], 1)
                 d["band_len_per_lane"] = d.get("band_scan_len", 0) / max(d["bounce_lanes"], 1)
+                nsteps = sum(d.get(f"wq_steps_{b}", 0) for b in (16, 32, 48, 64))
+                if nsteps:  # BUNDLE_WQ node steps by fill, and the share of the 4 member slots that are valid
+                    for b in (16, 32, 48, 64):
+                        d[f"wq_step_share_{b}"] = d[f"wq_steps_{b}"] / nsteps
+                    d["wq_pairs_per_node_step"] = d["bvh_visits"] / nsteps
+                    d["wq_member_use"] = d.get("wq_members", 0) / max(4 * d["bvh_visits"], 1)
                 print(json.dumps(d), flush=True)
                 ctx.set_option(_lib.OPT_COUNTERS, 1)
     out = []

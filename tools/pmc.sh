@@ -10,9 +10,9 @@ OUT=gpurun_out/$TAG; mkdir -p $OUT
 ARGS="--warmup 5 --steps 20 --cpu-seconds 0 --realtime-frames 0 $*"  # the driver's bench shape
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" \
-           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
+           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU" \
            "GRBM_GUI_ACTIVE GRBM_COUNT SQ_ACTIVE_INST_ANY SQ_WAIT_ANY" \
-           "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_LDS_BANK_CONFLICT"; do
+           "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- \
     python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i ($set) failed: $(tail -3 $OUT/p$i.log)"; exit 1; }

@@ -83,6 +83,18 @@ def summarise(passes, frames):
             d["executed_fp32_flops_per_launch"] = fl
             d["executed_fp32_flops_per_frame"] = fl / frames
             d["executed_fp32_tflops"] = fl / dur / 1e12
+        if "SQ_INSTS_VALU_FLOPS_FP32" in c:
+            # (tools/probe/flops_probe.hip, r05a: FLOPS_FP32 counts per WAVE-instruction -- fma 2, mul / add /
+            # trans 1 -- whatever the exec mask, i.e. the same as 2 FMA + MUL + ADD (+ TRANS) above / 64)
+            d["fp32_flops_counter_per_frame"] = 64 * c["SQ_INSTS_VALU_FLOPS_FP32"] / frames
+            d["fp32_trans_ops_counter_per_frame"] = 64 * c.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0) / frames
+        if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_ACTIVE_INST_VALU"):
+            # lanes active per VALU instruction (rocprof's VALUUtilization; r05b: exactly the exec mask's
+            # share on the probe), and the FP32 FLOPs the ACTIVE lanes execute at that share
+            d["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"])
+            if "executed_fp32_flops_per_frame" in d:
+                d["lane_fp32_flops_per_frame"] = d["executed_fp32_flops_per_frame"] * d["valu_lane_utilisation"]
+                d["lane_fp32_tflops"] = d["lane_fp32_flops_per_frame"] * frames / dur / 1e12
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             rd, wr = 2 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
             d.update(hbm_read_bytes_per_frame=rd / frames, hbm_write_bytes_per_frame=wr / frames,
@@ -134,6 +146,9 @@ def main():
                        "reference_tests_per_frame": ref_tests,
                        "executed_flops_per_reference_test": fl / ref_tests if fl and ref_tests else None,
                        "valu_issue_utilisation": d.get("valu_issue_utilisation"),
+                       "valu_lane_utilisation": d.get("valu_lane_utilisation"),
+                       "lane_fp32_flops_per_frame": d.get("lane_fp32_flops_per_frame"),
+                       "fp32_flops_counter_per_frame": d.get("fp32_flops_counter_per_frame"),
                        "wait_any_frac": d.get("wait_any_frac"),
                        "lds_conflict_cycles_per_lds_inst": d.get("lds_conflict_cycles_per_lds_inst"),
                        "counters_per_launch": d["counters_per_launch"],

@@ -1,10 +1,10 @@
 #!/bin/bash
-# r04 GPU session step: the GPU suite (unless SKIP_TESTS=1), smoke, optional interleaved A/B of library
+# GPU session step: the GPU suite (unless SKIP_TESTS=1), smoke, optional interleaved A/B of library
 # builds (AB_LIBS="libA libB ...", island and cave, AB_ROUNDS rounds), optional cull diagnostics of the
 # product library (DIAG=1) and the N=1 bench line (BENCH=1).
-# Usage (repo root, via gpurun): bash tools/r04.sh <tag>
+# Usage (repo root, via gpurun): bash tools/session.sh <tag>
 set -o pipefail
-TAG=${1:-r04a}
+TAG=${1:?usage: session.sh <tag>}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/gpu_tests.log; exit 1; }
