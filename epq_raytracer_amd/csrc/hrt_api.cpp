@@ -1418,7 +1418,7 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
         free_dev(ctx, ctx->timeline);
         free_dev(ctx, ctx->timeline_count);
       }
-      HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->timeline, (size_t)value * 3 * sizeof(unsigned long long)));
+      HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->timeline, (size_t)value * 4 * sizeof(unsigned long long)));
       HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->timeline_count, sizeof(uint32_t)));
       HRT_HIP(ctx, hipMemset(ctx->timeline_count, 0, sizeof(uint32_t)));
       ctx->timeline_cap = (uint32_t)value;
@@ -1441,7 +1441,7 @@ extern "C" hrt_status hrt_debug_timeline(hrt_context* ctx, uint64_t* out, uint32
   HRT_HIP(ctx, hipMemcpy(&n, ctx->timeline_count, sizeof n, hipMemcpyDeviceToHost));
   n = std::min(n, ctx->timeline_cap);
   *count = n;
-  HRT_HIP(ctx, hipMemcpy(out, ctx->timeline, (size_t)std::min(n, cap) * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HRT_HIP(ctx, hipMemcpy(out, ctx->timeline, (size_t)std::min(n, cap) * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return HRT_OK;
 }
 

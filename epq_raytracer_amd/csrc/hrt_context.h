@@ -138,7 +138,7 @@ struct hrt_context {
   int64_t debug_fail_alloc = 0;   // debug build: fail the n-th device allocation of the next hrt_set_scene
   uint32_t debug_grab_runs = 0;   // debug build: HRT_DEBUG_OPT_GRAB_RUNS
   uint32_t debug_wq_tri_cap = 0;  // debug build: HRT_DEBUG_OPT_WQ_TRI_CAP (triangle-pair stack capacity)
-  unsigned long long* timeline = nullptr;  // HRT_TIMELINE builds: HRT_DEBUG_OPT_TIMELINE records (3 u64 each)
+  unsigned long long* timeline = nullptr;  // HRT_TIMELINE builds: HRT_DEBUG_OPT_TIMELINE records (4 u64 each)
   uint32_t* timeline_count = nullptr;
   uint32_t timeline_cap = 0;
 

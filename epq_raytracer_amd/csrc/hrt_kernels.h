@@ -78,8 +78,8 @@ struct TraceParams {
   float bvh_band_a1;    // max over prims of |a|_1: the band's plane filter tolerance (bvh_band_nhat .w = n^.a)
   uint32_t grab_always; // (debug, HRT_DEBUG_OPT_GRAB_RUNS) persistent waves take kGrab items per atomic to the end
   // (builds with -DHRT_TIMELINE=1, HRT_DEBUG_OPT_TIMELINE) per executed work item of the persistent kernels:
-  // {s_memrealtime at its start, at its end, tile | log2 k << 22 | s << 25 | hot << 31 | frame << 32 |
-  // run << 40 | resident wave << 48}; timeline_count counts the records (capacity timeline_cap)
+  // {s_memrealtime at its start, when its tile list was built, at its end, tile | log2 k << 22 | s << 25 |
+  // hot << 31 | frame << 32 | run << 40 | sky << 47 | resident wave << 48}; timeline_count counts the records (capacity timeline_cap)
   unsigned long long* timeline;
   uint32_t* timeline_count;
   uint32_t timeline_cap;

@@ -30,6 +30,10 @@
 
 namespace hrt {
 
+#ifndef HRT_TIMELINE
+#define HRT_TIMELINE 0  // per-item timeline records (tools/timeline.py; A/B builds only)
+#endif
+
 
 #ifndef HRT_SHADE_KARGS
 #define HRT_SHADE_KARGS 1  // shading reads the scene pointers from the kernel arguments (kargs)
@@ -1109,6 +1113,10 @@ struct Coop {
   bool defer = false;
   unsigned long long acc_s = 0, acc_t = 0, acc_m = 0;
   bool hot = false;              // the item's wave runs at issue priority 3 (tile_loop)
+#if HRT_TIMELINE
+  unsigned long long t_setup = 0;  // s_memrealtime when the item's tile list was built (timeline builds)
+  unsigned long long t_sky = 0;    // ... 1 if the item ran as a sky item
+#endif
 };
 
 __device__ __forceinline__ void coop_merge(Coop& co, Closest& c) {
@@ -1501,9 +1509,6 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #endif
 #ifndef HRT_WQ_EARLY_REC
 #define HRT_WQ_EARLY_REC 1  // a node step's first member pair read before the slot read (r04)
-#endif
-#ifndef HRT_TIMELINE
-#define HRT_TIMELINE 0  // per-item timeline records (tools/timeline.py; A/B builds only)
 #endif
 #ifndef HRT_WQ_BAND_EARLY
 #define HRT_WQ_BAND_EARLY 0  // (r05b: neutral, island 1.786 / 1.787, cave 5.405 / 5.400 ms) a bounce lane's direction-cell offsets requested at the batch's start (r05)
@@ -2257,6 +2262,10 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
 #endif
   const TileList tl = build_tile_list(P, active, centre, list_lds);
+#if HRT_TIMELINE
+  co.t_setup = __builtin_amdgcn_s_memrealtime();
+  co.t_sky = tl.ok && tl.n == 0u && pc.num_spheres == 0;
+#endif
   // bounce batch threshold scaled to the item's active lanes (a split tile's row group has 8/k rows):
   // a batch of few lanes then runs alongside the other lanes' primary segments instead of after them
   const uint32_t sec_thresh = max(1u, (kargs()->sec_batch * (uint32_t)__popcll(__ballot(active)) + 63u) / 64u);
@@ -2637,11 +2646,13 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
       const uint32_t slot = atomicAdd(P.timeline_count, 1u);
       if (slot < P.timeline_cap) {
         const uint32_t wave = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
-        P.timeline[3 * (size_t)slot] = rt0;
-        P.timeline[3 * (size_t)slot + 1] = rt1;
-        P.timeline[3 * (size_t)slot + 2] = (unsigned long long)(tile | (lk << 22) | (sub << 25) | ((uint32_t)hot << 31)) |
+        P.timeline[4 * (size_t)slot] = rt0;
+        P.timeline[4 * (size_t)slot + 1] = solo.t_setup;
+        P.timeline[4 * (size_t)slot + 2] = rt1;
+        P.timeline[4 * (size_t)slot + 3] = (unsigned long long)(tile | (lk << 22) | (sub << 25) | ((uint32_t)hot << 31)) |
                                            ((unsigned long long)(tf & 0xFFu) << 32) |
-                                           ((unsigned long long)(run & 0xFFu) << 40) |
+                                           ((unsigned long long)(run & 0x7Fu) << 40) |
+                                           ((unsigned long long)(solo.t_sky & 1u) << 47) |
                                            ((unsigned long long)(wave & 0xFFFFu) << 48);
       }
     }
@@ -2705,6 +2716,7 @@ __global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves,
   sched[4] = heavy_items;  // the plan's first heavy_items items are the heavy tiles' (tile_loop grabs them singly)
   sched[3] = hb;
 }
+
 // Item word: tile | log2(items of the tile) << 22 | item index s << 25 | heavy << 31 (tile_loop).
 __global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t* cost, uint32_t tiles, uint32_t kmax,
                                                  uint32_t prio, uint32_t* items) {

@@ -507,8 +507,8 @@ hrt_status hrt_debug_band_flatten(int device, const uint32_t n[64], const uint32
 hrt_status hrt_debug_wq_protocol(int device, uint32_t rounds, const uint32_t* cnt, const uint32_t* take,
                                  const uint32_t* tgt, const uint64_t* val, const uint64_t seed[64], uint32_t* popped,
                                  uint64_t* seen, uint64_t slots[64], uint32_t* depth);
-/* HRT_TIMELINE builds: the last trace launch's item records (3 words each: start, end, item | frame << 32 |
- * run << 40 | wave << 48), at most cap of them copied; *count = the records the launch wrote (<= the
+/* HRT_TIMELINE builds: the last trace launch's item records (4 words each: start, tile list built, end,
+ * item | frame << 32 | run << 40 | sky << 47 | wave << 48), at most cap of them copied; *count = the records the launch wrote (<= the
  * HRT_DEBUG_OPT_TIMELINE capacity).  Other builds: HRT_ERR_INVALID_ARGUMENT. */
 hrt_status hrt_debug_timeline(hrt_context* ctx, uint64_t* out, uint32_t cap, uint32_t* count);
 hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);

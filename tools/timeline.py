@@ -5,8 +5,8 @@ last items finish), the heavy items' chains, the gaps between a wave's items.
     HRT_LIB=epq_raytracer_amd/build/ab_timeline/libhip_raytrace.so \\
         python tools/timeline.py [--partition 8,6,8] [--steps 20] [--warmup 5] [--json out.json]
 
-Records (hip_raytrace.h HRT_DEBUG_OPT_TIMELINE): start, end (s_memrealtime, 100 MHz), item word | frame << 32 |
-run << 40 | resident wave << 48.
+Records (hip_raytrace.h HRT_DEBUG_OPT_TIMELINE): start, tile list built, end (s_memrealtime, 100 MHz), item word |
+frame << 32 | run << 40 | sky << 47 | resident wave << 48.
 """
 import argparse
 import ctypes
@@ -26,23 +26,26 @@ TICK_US = 0.01  # s_memrealtime: 100 MHz
 
 
 def records(ctx, cap):
-    out = np.zeros(3 * cap, np.uint64)
+    out = np.zeros(4 * cap, np.uint64)
     n = ctypes.c_uint32(0)
     _lib.check(ctx.lib.hrt_debug_timeline(ctx.handle, _lib.ptr(out), cap, ctypes.byref(n)), "hrt_debug_timeline",
                ctx.handle, ctx.lib)
-    r = out[: 3 * min(n.value, cap)].reshape(-1, 3)
+    r = out[: 4 * min(n.value, cap)].reshape(-1, 4)
     return r, n.value
 
 
 def analyse(r, waves):
     t0 = int(r[:, 0].min())
     s = (r[:, 0].astype(np.int64) - t0) * TICK_US
-    e = (r[:, 1].astype(np.int64) - t0) * TICK_US
-    w = r[:, 2]
+    su = (r[:, 1].astype(np.int64) - t0) * TICK_US
+    e = (r[:, 2].astype(np.int64) - t0) * TICK_US
+    w = r[:, 3]
+    sky = ((w >> 47) & 1).astype(bool)
+    setup = su - s
     item = (w & 0xFFFFFFFF).astype(np.uint64)
     hot = ((item >> 31) & 1).astype(bool)
     lk = ((item >> 22) & 7).astype(int)
-    run = ((w >> 40) & 0xFF).astype(int)
+    run = ((w >> 40) & 0x7F).astype(int)
     wave = ((w >> 48) & 0xFFFF).astype(int)
     span = float(e.max())
     dur = e - s
@@ -84,12 +87,23 @@ def analyse(r, waves):
                   "dur_us_max": round(float(dur[heavy].max()), 1) if heavy.any() else None,
                   "start_us_max": round(float(s[heavy].max()), 1) if heavy.any() else None,
                   "end_us_max": round(float(e[heavy].max()), 1) if heavy.any() else None},
+        "tile_frames": int(run.sum()),
+        "wave_us_per_tile_frame": {"all": round(float(dur.sum()) / max(int(run.sum()), 1), 2),
+                                   "setup": round(float(setup.sum()) / max(int(run.sum()), 1), 2),
+                                   "sky": round(float(dur[sky].sum()) / max(int(run.sum()), 1), 2),
+                                   "nonsky": round(float(dur[~sky].sum()) / max(int(run.sum()), 1), 2)},
+        "setup_us": {"p50": round(float(np.percentile(setup, 50)), 2), "mean": round(float(setup.mean()), 2),
+                     "p99": round(float(np.percentile(setup, 99)), 2)},
+        "sky_items": int(sky.sum()), "sky_runs_mean": round(float(run[sky].mean()), 2) if sky.any() else None,
+        "nonsky_runs_mean": round(float(run[~sky].mean()), 2) if (~sky).any() else None,
+        "nonsky_dur_us": {"p50": round(float(np.percentile(dur[~sky], 50)), 1),
+                          "p99": round(float(np.percentile(dur[~sky], 99)), 1)} if (~sky).any() else None,
         "light": {"items": int((~heavy).sum()), "dur_us_p50": round(float(np.percentile(dur[~heavy], 50)), 1),
                   "dur_us_p99": round(float(np.percentile(dur[~heavy], 99)), 1),
                   "dur_us_max": round(float(dur[~heavy].max()), 1), "runs_mean": round(float(run[~heavy].mean()), 2)},
         "last_items": [{"end_us": round(float(e[i]), 1), "start_us": round(float(s[i]), 1),
                         "tile": int(item[i] & 0x3FFFFF), "lk": int(lk[i]), "hot": bool(hot[i]),
-                        "frame": int((w[i] >> 32) & 0xFF), "run": int(run[i])} for i in last],
+                        "frame": int((w[i] >> 32) & 0xFF), "run": int(run[i]), "sky": bool(sky[i])} for i in last],
         "busy_frac_curve": [round(float(v), 3) for v in frac[::10]],
     }
 
@@ -107,6 +121,7 @@ def main():
     ap.add_argument("--cap", type=int, default=1 << 20)
     ap.add_argument("--option", type=lambda s: tuple(int(v) for v in s.split("=")), action="append", default=[])
     ap.add_argument("--json", default=None)
+    ap.add_argument("--raw", default=None, help="also save the raw records (.npy)")
     a = ap.parse_args()
     W, H = a.width, a.height
     camera, settings = E.preset(a.scene)
@@ -128,12 +143,13 @@ def main():
     ctx.synchronize()
     st = ctx.stats()
     r, n = records(ctx, a.cap)
-    import torch  # noqa: F401  (device properties only)
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if a.raw:
+        np.save(a.raw, r)
+    waves = int(((r[:, 3] >> 48) & 0xFFFF).max()) + 1 if len(r) else 1  # resident waves (each takes an item)
     res = {"scene": a.scene, "partition": a.partition, "frames": a.steps, "options": a.option,
            "kernel_ms_per_frame": round(st.total_trace_ms / max(st.traces, 1), 4),
            "launch_ms": round(st.total_trace_ms / max(st.traces, 1) * a.steps, 3), "records": n,
-           **analyse(r, cus * 16)}
+           **analyse(r, waves)}
     ctx.close()
     print(json.dumps(res), flush=True)
     if a.json:
