@@ -17,3 +17,7 @@ timeout -k 10 300 python3 bench.py --gpus 2 --dist-backend gloo --steps 16 --war
 cat $OUT/bench_n2_gloo.json
 timeout -k 10 600 bash tools/configs_round.sh > $OUT/configs.txt 2>&1 || { echo "configs failed"; tail -5 $OUT/configs.txt; exit 1; }
 cat $OUT/configs.txt
+timeout -k 10 300 python3 tools/rank_shape.py --rounds 2 > $OUT/rank8_bench_shape.jsonl 2>&1 || { echo "rank shape failed"; tail -5 $OUT/rank8_bench_shape.jsonl; exit 1; }
+tail -1 $OUT/rank8_bench_shape.jsonl
+timeout -k 10 300 python3 tools/rank_shape.py --rounds 1 --scene cave > $OUT/rank8_bench_shape_cave.jsonl 2>&1 || { echo "cave rank shape failed"; tail -5 $OUT/rank8_bench_shape_cave.jsonl; exit 1; }
+tail -1 $OUT/rank8_bench_shape_cave.jsonl
