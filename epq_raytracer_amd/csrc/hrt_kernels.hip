@@ -2918,10 +2918,43 @@ __device__ __forceinline__ float4 combine_rgba32f(float4 p, float4 n, uint32_t f
   const float ff = (float)frame, ff1 = (float)(frame + 1u);
   return make_float4((n.x + p.x * ff) / ff1, (n.y + p.y * ff) / ff1, (n.z + p.z * ff) / ff1, 1.0f);
 }
+// combine_rgba8 with its nine IEEE divisions replaced by the same quotients (r05): the six UNORM8 loads
+// k / 255 from a 256-entry table of those quotients (unorm8_to_float, built once per workgroup in LDS),
+// and the three divisions by frame + 1 through that denominator's reciprocal, shared by the channels
+// (div_core: rcp_core is RN(1 / b) on [2^-40, 2^40], every numerator here is 0 or in [2^-8, 2^33], so
+// Markstein's correction gives the correctly rounded quotient; a zero numerator gives +0 as the IEEE
+// division does).  combine_rgba8 stays the reference spelling (tests/test_gpu_parity.py holds every
+// accumulator to the oracle's combiner).
+__device__ __forceinline__ uint32_t combine_rgba8_fast(uint32_t pv, uint32_t nv, uint32_t frame, const float* tab) {
+  if (frame == 0) return 255u << 24;
+  const float ff = (float)frame, ff1 = (float)(frame + 1u), y = rcp_core(ff1);
+  uint32_t out = 255u << 24;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const float prev = tab[(pv >> (8 * ch)) & 255u];
+    const float nc = tab[(nv >> (8 * ch)) & 255u];
+    out |= unorm8(div_core(nc + prev * ff, ff1, y)) << (8 * ch);
+  }
+  return out;
+}
+#ifndef HRT_COMBINE_FAST
+#define HRT_COMBINE_FAST 1
+#endif
+__device__ __forceinline__ void unorm8_table(float* tab) {  // blockDim.x == 256
+  tab[threadIdx.x] = unorm8_to_float(threadIdx.x);
+  __syncthreads();
+}
 __global__ __launch_bounds__(256) void accumulate_rgba8(uint32_t* cur, const uint32_t* nw, size_t npix, uint32_t frame) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+#if HRT_COMBINE_FAST
+  __shared__ float tab[256];
+  unorm8_table(tab);
+  if (i >= npix) return;
+  cur[i] = combine_rgba8_fast(frame == 0 ? 0u : cur[i], nw[i], frame, tab);
+#else
   if (i >= npix) return;
   cur[i] = combine_rgba8(frame == 0 ? 0u : cur[i], nw[i], frame);
+#endif
 }
 // hrt_compute_n: the nf frames of one launch folded in frame order in one pass (frame frame0 + f is
 // image f of the stack): the per-frame combiner's arithmetic, pixel by pixel, with the accumulator
@@ -2929,9 +2962,17 @@ __global__ __launch_bounds__(256) void accumulate_rgba8(uint32_t* cur, const uin
 __global__ __launch_bounds__(256) void accumulate_frames_rgba8(uint32_t* cur, const uint32_t* stack, size_t npix,
                                                              uint32_t nf, uint32_t frame0) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+#if HRT_COMBINE_FAST
+  __shared__ float tab[256];
+  unorm8_table(tab);
+#endif
   if (i >= npix) return;
   uint32_t v = cur[i];
+#if HRT_COMBINE_FAST
+  for (uint32_t f = 0; f < nf; ++f) v = combine_rgba8_fast(v, stack[f * npix + i], frame0 + f, tab);
+#else
   for (uint32_t f = 0; f < nf; ++f) v = combine_rgba8(v, stack[f * npix + i], frame0 + f);
+#endif
   cur[i] = v;
 }
 __global__ __launch_bounds__(256) void accumulate_frames_rgba32f(float4* cur, const float4* stack, size_t npix,
