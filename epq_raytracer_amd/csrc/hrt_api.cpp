@@ -330,6 +330,8 @@ extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_
       return bail(hip_fail(ctx, e, "hipMalloc(tile costs)"));
     if ((e = hrt::dev_alloc(ctx, (void**)&l.item_buf, tiles * 64 * 4)) != hipSuccess)
       return bail(hip_fail(ctx, e, "hipMalloc(items)"));
+    if ((e = hrt::dev_alloc(ctx, (void**)&l.tl_cache, tiles * hrt::kTlRecWords * 4)) != hipSuccess)
+      return bail(hip_fail(ctx, e, "hipMalloc(tile lists)"));
   }
   if (ctx->mode == HRT_MODE_RGBA8)
     e = hrt::dev_alloc(ctx, (void**)&ctx->accum8, np * 4);
@@ -374,6 +376,7 @@ extern "C" void hrt_destroy(hrt_context* ctx) {
     free_dev(ctx, l.sched);
     free_dev(ctx, l.tile_cost);
     free_dev(ctx, l.item_buf);
+    free_dev(ctx, l.tl_cache);
     if (l.done) (void)hipEventDestroy(l.done);
     if (l.free) (void)hipEventDestroy(l.free);
     if (l.stream) (void)hipStreamDestroy(l.stream);
@@ -598,7 +601,7 @@ extern "C" hrt_status hrt_set_scene(hrt_context* ctx, const hrt_ray* rays, uint3
   ctx->scene = s;
   ctx->debug_fail_alloc = 0;
   if (!keep_rays) ctx->n_rays = n_rays;
-  for (auto& l : ctx->lane) l.plan_valid = l.cam_ready = false;  // costs and camera lists of the old scene
+  for (auto& l : ctx->lane) l.plan_valid = l.cam_ready = l.tl_ready = false;  // costs, camera and tile lists of the old scene
   ctx->scene_set = true;
   return HRT_OK;
 }
@@ -646,6 +649,7 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.sched = lane.sched;
   p.tile_cost = lane.tile_cost;
   p.item_buf = lane.item_buf;
+  p.tl_cache = lane.tl_cache;
   p.split_k = ctx->split_k;
   p.split_factor = ctx->split_factor;
   p.split_prio = ctx->split_prio;
@@ -730,6 +734,17 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stre
   key[3] = p.pc.num_meshes;
   p.cam_lists_ready = lane.cam_ready && std::memcmp(key, lane.cam_key, sizeof key) == 0 ? 1u : 0u;
   lane.cam_ready = false;  // until a launch has rebuilt them
+  // the persistent kernels' tile lists (tile_lists): a function of the camera (position, the mat3 the
+  // kernels read, jitter), the meshes and the ray centres -- rebuilt when the camera differs from the one
+  // they were built for, after hrt_set_scene or hrt_generate_rays, and after a launch of another kernel
+  uint32_t tkey[14];
+  std::memcpy(tkey, p.pc.cam_pos, 12);
+  for (int i = 0, j = 0; i < 11; ++i)
+    if (i % 4 != 3) std::memcpy(&tkey[3 + j++], &p.pc.cam_alignment_mat[i], 4);
+  std::memcpy(&tkey[12], &p.pc.jitter_size, 4);
+  tkey[13] = p.pc.num_meshes;
+  p.tl_lists_ready = lane.tl_ready && std::memcmp(tkey, lane.tl_key, sizeof tkey) == 0 ? 1u : 0u;
+  lane.tl_ready = false;
   if (ctx->probe && !lane.plan_valid && ctx->num_tiles() >= 1024 && persistent_kernel(resolved)) {
     hrt::TraceParams q = p;
     q.pc.num_samples = 1;
@@ -747,6 +762,7 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stre
     }
     p.plan_valid = 1u;
     if (builds_camera_lists(ran)) p.cam_lists_ready = 1u;  // the probe built them
+    if (persistent_kernel(ran)) p.tl_lists_ready = 1u;     // (and the tile lists)
   }
   HRT_HIP(ctx, hipEventRecord(ev.start, stream));
   hipError_t e = hrt::launch_trace(p, variant, stream, &ctx->last_kernel, &ctx->last_block);
@@ -758,6 +774,10 @@ hrt_status launch_frames(hrt_context* ctx, hrt::TraceParams& p, hipStream_t stre
   if (e == hipSuccess && builds_camera_lists(ctx->last_kernel)) {
     lane.cam_ready = true;
     std::memcpy(lane.cam_key, key, sizeof key);
+  }
+  if (e == hipSuccess && persistent_kernel(ctx->last_kernel)) {
+    lane.tl_ready = true;
+    std::memcpy(lane.tl_key, tkey, sizeof tkey);
   }
   if (e != hipSuccess) {
     ctx->event_pool.push_back(ev);
@@ -1075,6 +1095,7 @@ extern "C" hrt_status hrt_generate_rays(hrt_context* ctx, float camera_focal_len
     ctx->n_rays = 0;
     HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->scene.rays, (want ? want : 1) * sizeof(float4)));
   }
+  for (auto& l : ctx->lane) l.tl_ready = false;  // the tile lists were built from the old ray centres
   if (n) HRT_HIP(ctx, hrt::launch_make_rays(ctx->scene.rays, ctx->width, ctx->height, first, px, py, ctx->stream));
   HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->n_rays = (uint32_t)want;

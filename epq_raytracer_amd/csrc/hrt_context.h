@@ -76,11 +76,14 @@ struct Lane {
   uint32_t* sched = nullptr;      // persistent kernels' scheduler words (hrt_kernels.h)
   uint32_t* tile_cost = nullptr;  // per 8x8 tile
   uint32_t* item_buf = nullptr;   // planned work items (tiles x 64)
+  uint32_t* tl_cache = nullptr;   // the persistent kernels' whole-tile lists (tiles x hrt::kTlRecWords, tile_lists)
   bool plan_valid = false;        // tile_cost describes this lane's last trace (same scene)
   // the lane's camera lists (camera_lists) hold the records of this camera position (same scene):
   // a trace from the same position skips rebuilding them
   bool cam_ready = false;
   uint32_t cam_key[4] = {};       // cam_pos bits, num_meshes
+  bool tl_ready = false;          // tl_cache holds the tile lists of tl_key's camera (tile_lists ran)
+  uint32_t tl_key[14] = {};       // cam_pos, mat3 of cam_alignment_mat, jitter_size bits, num_meshes
   hipEvent_t done = nullptr;      // recorded on `stream` after each trace / clear of the lane
   hipEvent_t free = nullptr;      // recorded on the context stream after the lane's last reader
   bool done_set = false, free_set = false;

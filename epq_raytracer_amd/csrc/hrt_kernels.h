@@ -83,7 +83,13 @@ struct TraceParams {
   unsigned long long* timeline;
   uint32_t* timeline_count;
   uint32_t timeline_cap;
+  // persistent kernels (HRT_TL_PREPASS): per 8x8 tile of this launch, the wave's primary triangle list and
+  // octant table as build_tile_list makes them (kTlRecWords words: list entries per lane, octant test sums
+  // per lane, n, ok, aabb lo / hi, aabb_ok), filled by the tile_lists kernel before the trace; nullptr = off
+  uint32_t* tl_cache;
+  uint32_t tl_lists_ready;  // tl_cache already holds this camera's lists (hrt_api.cpp launch_frames): no tile_lists
 };
+constexpr uint32_t kTlRecWords = 136;
 
 // Per device, once: the dynamic-LDS limits of the persistent kernels (hipFuncSetAttribute).
 hipError_t ensure_kernel_attributes(int device);

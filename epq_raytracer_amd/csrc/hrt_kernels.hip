@@ -33,6 +33,9 @@ namespace hrt {
 #ifndef HRT_TIMELINE
 #define HRT_TIMELINE 0  // per-item timeline records (tools/timeline.py; A/B builds only)
 #endif
+#ifndef HRT_TL_PREPASS
+#define HRT_TL_PREPASS 1  // the persistent kernels' whole-tile lists built once per launch (tile_lists, r05)
+#endif
 
 
 #ifndef HRT_SHADE_KARGS
@@ -1113,6 +1116,7 @@ struct Coop {
   bool defer = false;
   unsigned long long acc_s = 0, acc_t = 0, acc_m = 0;
   bool hot = false;              // the item's wave runs at issue priority 3 (tile_loop)
+  uint32_t cache_tile = 0xFFFFFFFFu;  // a whole tile's item: its tile (the launch's tile_lists record), else ~0
 #if HRT_TIMELINE
   unsigned long long t_setup = 0;  // s_memrealtime when the item's tile list was built (timeline builds)
   unsigned long long t_sky = 0;    // ... 1 if the item ran as a sky item
@@ -2261,7 +2265,29 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
 #if !HRT_RAYGEN_KARGS
   const f3 root = mk(pc.cam_pos[0], pc.cam_pos[1], pc.cam_pos[2]);
 #endif
+#if HRT_TL_PREPASS
+  // a whole tile's item: the list the launch's tile_lists kernel built for the tile (the same function of
+  // the same inputs -- camera, the tile's ray centres, the camera lists -- as building it here, which the
+  // launch's other frames of the tile would repeat; r05c timelines: ~11 us of dependent L2 round trips
+  // per item, 6 wave-us per tile-frame on island, 13 on a rank of 8)
+  TileList tl;
+  if (co.cache_tile != 0xFFFFFFFFu && !list_lds) {
+    const uint32_t* rec = kargs()->tl_cache + (size_t)co.cache_tile * kTlRecWords;
+    const uint32_t lane = threadIdx.x & 63;
+    tl.v = rec[lane];
+    tl.tsum = rec[64 + lane];
+    tl.lds = nullptr;
+    tl.n = __builtin_amdgcn_readfirstlane(rec[128]);
+    tl.ok = __builtin_amdgcn_readfirstlane(rec[129]) != 0u;
+    tl.aabb = (unsigned long long)__builtin_amdgcn_readfirstlane(rec[130]) |
+              ((unsigned long long)__builtin_amdgcn_readfirstlane(rec[131]) << 32);
+    tl.aabb_ok = __builtin_amdgcn_readfirstlane(rec[132]) != 0u;
+  } else {
+    tl = build_tile_list(P, active, centre, list_lds);
+  }
+#else
   const TileList tl = build_tile_list(P, active, centre, list_lds);
+#endif
 #if HRT_TIMELINE
   co.t_setup = __builtin_amdgcn_s_memrealtime();
   co.t_sky = tl.ok && tl.n == 0u && pc.num_spheres == 0;
@@ -2638,6 +2664,7 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
     if (hot) __builtin_amdgcn_s_setprio(3);
     solo.hot = hot;
     solo.work = 0;
+    solo.cache_tile = (HRT_TL_PREPASS && K->tl_cache && lk == 0u) ? tile : 0xFFFFFFFFu;
     body(x, lr, solo, tf, run);
     if (hot) __builtin_amdgcn_s_setprio(0);
 #if HRT_TIMELINE
@@ -2807,6 +2834,37 @@ __global__ __launch_bounds__(1024) void trace_bundle_bvh_lds(TraceParams P) {
     trace_fused_split<kBounceBvh, D>(P, x, lr, CullGlobal{T, to_const(T)}, BvhLds{nodes, lds_tris, entries, kbase},
                                      nullptr, co, f, nr);
   });
+}
+
+// The persistent kernels' whole-tile lists (HRT_TL_PREPASS): one wave per 8x8 tile builds exactly what
+// trace_fused_split's build_tile_list would for the tile's whole-tile items (the same pixels, the same
+// function) and stores it in the tile's record; the launch's items of the tile then read it back (every
+// frame of a multi-frame launch shares the camera and the camera lists).
+__global__ __launch_bounds__(256) void tile_lists(TraceParams P) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t tiles_x = (P.pc.width + 7) / 8, tiles = tiles_x * ((P.local_rows + 7) / 8);
+  const uint32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= tiles) return;  // wave-uniform
+  const uint32_t ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const uint32_t x = tx * 8 + (lane & 7), lr = ty * 8 + (lane >> 3);
+  const uint32_t y = global_row(lr, P);
+  const bool active = x < P.pc.width && lr < P.local_rows && y < P.pc.height;
+  f3 centre = mk(0.0f, 0.0f, 0.0f);
+  if (active) {
+    const float4 rc = P.rays[x + y * P.pc.width];
+    centre = mk(rc.x, rc.y, rc.z);
+  }
+  const TileList t = build_tile_list(P, active, centre, nullptr);
+  uint32_t* rec = P.tl_cache + (size_t)tile * kTlRecWords;
+  rec[lane] = t.v;
+  rec[64 + lane] = t.tsum;
+  if (lane == 0) {
+    rec[128] = t.n;
+    rec[129] = t.ok ? 1u : 0u;
+    rec[130] = (uint32_t)t.aabb;
+    rec[131] = (uint32_t)(t.aabb >> 32);
+    rec[132] = t.aabb_ok ? 1u : 0u;
+  }
 }
 
 // Per-frame prep for the bundle variants: one workgroup per mesh, order-preserving compaction of the
@@ -3311,6 +3369,7 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
     }
     case HRT_KERNEL_BUNDLE_BVH_LDS: {
       if (p.pc.num_meshes > 0 && !p.cam_lists_ready) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      if (HRT_TL_PREPASS && p.tl_cache && !p.tl_lists_ready) tile_lists<<<(tiles_of(p) + 3) / 4, 256, 0, stream>>>(p);
       TraceParams q = p;
       q.coop = 0;
       if (q.split_k == 0) q.split_k = 1;
@@ -3325,6 +3384,7 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
     }
     case HRT_KERNEL_BUNDLE_WQ: {
       if (p.pc.num_meshes > 0 && !p.cam_lists_ready) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      if (HRT_TL_PREPASS && p.tl_cache && !p.tl_lists_ready) tile_lists<<<(tiles_of(p) + 3) / 4, 256, 0, stream>>>(p);
       TraceParams q = p;
       q.coop = 0;
       // auto: a pair step's work scales with the rays in the batch, so heavy tiles (> factor x a
@@ -3353,6 +3413,7 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
     }
     case HRT_KERNEL_BUNDLE_CULL_LDS: {
       if (p.pc.num_meshes > 0 && !p.cam_lists_ready) camera_lists<<<p.pc.num_meshes, 256, 0, stream>>>(p);
+      if (HRT_TL_PREPASS && p.tl_cache && !p.tl_lists_ready) tile_lists<<<(tiles_of(p) + 3) / 4, 256, 0, stream>>>(p);
       TraceParams q = p;
       const uint32_t block = lds_block(p.n_tris);
       *block_out = (int)block;

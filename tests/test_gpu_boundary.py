@@ -451,6 +451,61 @@ def test_camera_lists_follow_the_camera(overlap):
     ctx.close()
 
 
+@pytest.mark.parametrize("overlap", [1, 3])
+def test_tile_lists_follow_camera_jitter_and_rays(overlap):
+    """The persistent kernels' tile lists (tile_lists, built once and kept while the camera stays): a path
+    through direction-only changes (the view matrix), a jitter change, back to the first camera, and a
+    re-generated ray buffer (hrt_generate_rays with another focal length) gives each trace exactly the
+    image of a fresh context with that camera and those rays.  1080p-sized tile counts are not needed:
+    96x72 tiles run the same kernels (the probe is off below 1,024 tiles)."""
+    case = SceneCase("island", (96, 72), 2, 4)
+    s = case.settings
+
+    def push(k, direction=None, jitter=None):
+        pc = case.push(k)
+        if direction is not None:
+            pc.cam_alignment_mat[:] = [float(v) for v in E.view_matrix(direction, case.camera.up)]
+        if jitter is not None:
+            pc.jitter_size = jitter
+        return pc
+
+    d0 = np.asarray(case.camera.direction, np.float32)
+    d1 = d0 + np.float32([0.05, -0.03, 0.02])
+    d2 = d0 + np.float32([-0.04, 0.02, 0.0])
+    path = [(1, None, None), (2, d1, None), (3, d2, None), (4, d2, case.jitter * 3.0), (5, None, None),
+            (6, None, None)]
+
+    def fresh(pc, focal):
+        ctx = E.HrtContext(case.size, device=0)
+        ctx.generate_rays(focal, s.viewport_height, s.up)
+        ctx.set_scene(None, case.spheres, case.tris, case.meshes)
+        ctx.trace(pc)
+        img = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+        ctx.close()
+        return img
+
+    ctx = E.HrtContext(case.size, device=0)
+    ctx.set_option(_lib.OPT_OVERLAP, overlap)
+    ctx.generate_rays(s.camera_focal_length, s.viewport_height, s.up)
+    ctx.set_scene(None, case.spheres, case.tris, case.meshes)
+    for k, direction, jitter in path:
+        pc = push(k, direction, jitter)
+        ctx.trace(pc)
+        got = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+        want = fresh(pc, s.camera_focal_length)
+        assert np.array_equal(got, want), f"frame {k}: {mismatch_report(got, want)}"
+    # new ray centres from the same camera: the lists must follow the rays (the camera key is unchanged)
+    # (no hrt_set_scene in between: hrt_generate_rays alone must drop the lists built from the old rays)
+    focal2 = s.camera_focal_length * 1.5
+    ctx.generate_rays(focal2, s.viewport_height, s.up)
+    pc = push(7)
+    ctx.trace(pc)
+    got = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+    want = fresh(pc, focal2)
+    ctx.close()
+    assert np.array_equal(got, want), f"regenerated rays: {mismatch_report(got, want)}"
+
+
 def test_camera_lists_after_a_variant_switch():
     """A kernel that neither builds nor reads the camera lists (LITERAL, BRUTE) leaves the lane's lists as
     they were: BUNDLE_WQ from position B, then LITERAL from A, then BUNDLE_WQ from A on the same lane must
