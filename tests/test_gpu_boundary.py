@@ -451,13 +451,17 @@ def test_camera_lists_follow_the_camera(overlap):
     ctx.close()
 
 
-@pytest.mark.parametrize("overlap", [1, 3])
-def test_tile_lists_follow_camera_jitter_and_rays(overlap):
+@pytest.mark.parametrize("overlap,split", [(1, 1), (3, 1), (1, 0)])
+def test_tile_lists_follow_camera_jitter_and_rays(overlap, split):
     """The persistent kernels' tile lists (tile_lists, built once and kept while the camera stays): a path
     through direction-only changes (the view matrix), a jitter change, back to the first camera, and a
     re-generated ray buffer (hrt_generate_rays with another focal length) gives each trace exactly the
     image of a fresh context with that camera and those rays.  1080p-sized tile counts are not needed:
-    96x72 tiles run the same kernels (the probe is off below 1,024 tiles)."""
+    96x72 tiles run the same kernels (the probe is off below 1,024 tiles); a long focal length keeps each
+    tile's ray cone as narrow as a 1080p tile's, so that its list fits (kTileCapVgpr) and is used -- at the
+    preset's focal length the 96x72 tiles' lists overflow and every tile takes the list-free path.  The
+    kept lists serve whole-tile items only: with 108 tiles against 4,096 resident waves the planner splits
+    every tile from the second trace on (HRT_OPT_SPLIT auto), so split = 1 keeps the tiles whole."""
     case = SceneCase("island", (96, 72), 2, 4)
     s = case.settings
 
@@ -469,10 +473,14 @@ def test_tile_lists_follow_camera_jitter_and_rays(overlap):
             pc.jitter_size = jitter
         return pc
 
+    # (changes large enough that a list kept from the previous camera misses triangles: a kept list that
+    # is a superset of the right one gives the right image, so small moves would not test the key --
+    # tools/exp/r05_tile_list_key_mutant.patch must fail here)
     d0 = np.asarray(case.camera.direction, np.float32)
-    d1 = d0 + np.float32([0.05, -0.03, 0.02])
-    d2 = d0 + np.float32([-0.04, 0.02, 0.0])
-    path = [(1, None, None), (2, d1, None), (3, d2, None), (4, d2, case.jitter * 3.0), (5, None, None),
+    c, sn = np.float32(np.cos(0.5)), np.float32(np.sin(0.5))
+    d1 = np.float32([c * d0[0] + sn * d0[2], d0[1], -sn * d0[0] + c * d0[2]])   # yaw +0.5 rad
+    d2 = np.float32([c * d0[0] - sn * d0[2], d0[1] * 0.6, sn * d0[0] + c * d0[2]])  # yaw -0.5 rad, tilt up
+    path = [(1, d2, None), (2, d1, None), (3, d2, None), (4, d2, case.jitter * 8.0), (5, None, None),
             (6, None, None)]
 
     def fresh(pc, focal):
@@ -486,17 +494,19 @@ def test_tile_lists_follow_camera_jitter_and_rays(overlap):
 
     ctx = E.HrtContext(case.size, device=0)
     ctx.set_option(_lib.OPT_OVERLAP, overlap)
-    ctx.generate_rays(s.camera_focal_length, s.viewport_height, s.up)
+    ctx.set_option(_lib.OPT_SPLIT, split)
+    focal = s.camera_focal_length * 12.0
+    ctx.generate_rays(focal, s.viewport_height, s.up)
     ctx.set_scene(None, case.spheres, case.tris, case.meshes)
     for k, direction, jitter in path:
         pc = push(k, direction, jitter)
         ctx.trace(pc)
         got = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
-        want = fresh(pc, s.camera_focal_length)
+        want = fresh(pc, focal)
         assert np.array_equal(got, want), f"frame {k}: {mismatch_report(got, want)}"
     # new ray centres from the same camera: the lists must follow the rays (the camera key is unchanged)
     # (no hrt_set_scene in between: hrt_generate_rays alone must drop the lists built from the old rays)
-    focal2 = s.camera_focal_length * 1.5
+    focal2 = focal * 0.5  # a wider view: the old lists miss the new edge pixels' triangles
     ctx.generate_rays(focal2, s.viewport_height, s.up)
     pc = push(7)
     ctx.trace(pc)
