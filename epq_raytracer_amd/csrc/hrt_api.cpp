@@ -513,12 +513,14 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
   // the LDS stacks kAutoLeafWqStack entries (island: 2; cave: 3, whose leaves of 2 need 104 KB of
   // nodes); 4 above 8192 entries
   uint32_t leaf = ctx->bvh_leaf ? ctx->bvh_leaf : hrt::auto_leaf_size(cap);
-  bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, bvh, ctx->bvh_width);
+  // (the hierarchy alone while the leaf size is chosen, then the band lists once)
+  bool built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, bvh, ctx->bvh_width, hrt::kBandTau, false);
   while (built && ctx->bvh_leaf == 0 && leaf < 4 &&
          !(bvh.wq_ok && hrt::wq_stack_cap(bvh.wq_n_nodes, bvh.wq_width, leaf) >= hrt::kAutoLeafWqStack)) {
     ++leaf;
-    built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, bvh, ctx->bvh_width);
+    built = hrt::build_bvh(tris, n_tris, meshes, n_meshes, leaf, bvh, ctx->bvh_width, hrt::kBandTau, false);
   }
+  if (built) hrt::build_bands(bvh);
   const double margin_frac = bvh.margin_frac;
   if (built) {
     auto up = [&](auto*& dst, const auto& v, const char* what) -> hrt_status {

@@ -7,6 +7,9 @@
 #include <atomic>
 #include <cmath>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <thread>
 
 #ifndef HRT_BVH_SWEEP
@@ -304,57 +307,6 @@ bool cone_hits_band(const Cone& k, V3 nhat, double tau) {
   return hi > -(tau + 1e-5) && lo < 2e-5;
 }
 
-// The cell itself (a convex spherical quad): corners in order and its edges' planes.  The exact range
-// of d.nhat over the quad is at a corner, at an edge's interior critical point (nhat projected onto
-// the edge's great circle, when that point lies on the edge), or +-1 when +-nhat lies inside.
-struct Quad {
-  V3 c[4], m[4];  // unit corners; m[i] = c[i] x c[i+1] (the edge's plane, unnormalized)
-  double s[4];    // +1 / -1: the side of plane i the quad lies on
-};
-Quad cell_quad(int f, double u0, double u1, double v0, double v1) {
-  Quad q;
-  const double us[4] = {u0, u1, u1, u0}, vs[4] = {v0, v0, v1, v1};
-  for (int i = 0; i < 4; ++i) {
-    q.c[i] = face_dir(f, us[i], vs[i]);
-    q.c[i] = q.c[i] * (1.0 / norm(q.c[i]));
-  }
-  V3 ctr = face_dir(f, 0.5 * (u0 + u1), 0.5 * (v0 + v1));
-  for (int i = 0; i < 4; ++i) {
-    q.m[i] = cross(q.c[i], q.c[(i + 1) & 3]);
-    q.s[i] = dot(q.m[i], ctr) >= 0.0 ? 1.0 : -1.0;
-  }
-  return q;
-}
-// Is d.nhat in the grazing band (-tau - 1e-5, 2e-5) for some d of the quad widened by 1e-4 rad
-// (the kernel's dir_cell rounding; moving d by an angle e moves d.nhat by at most e)?
-bool quad_hits_band(const Quad& q, V3 n, double tau) {
-  double hi = -2.0, lo = 2.0;
-  for (int i = 0; i < 4; ++i) {
-    const double v = dot(q.c[i], n);
-    hi = std::max(hi, v);
-    lo = std::min(lo, v);
-  }
-  bool in_p = true, in_m = true;
-  for (int i = 0; i < 4; ++i) {
-    const V3 a = q.c[i], b = q.c[(i + 1) & 3], m = q.m[i];
-    const double mm = dot(m, m);
-    const double side = q.s[i] * dot(m, n);
-    in_p = in_p && side >= 0.0;
-    in_m = in_m && side <= 0.0;
-    if (!(mm > 0.0)) continue;
-    const V3 pr = n - m * (dot(n, m) / mm);  // nhat projected onto the edge's great-circle plane
-    const double pl = norm(pr);
-    if (!(pl > 1e-12)) continue;
-    const V3 ph = pr * (1.0 / pl);
-    if (dot(cross(a, ph), m) >= 0.0 && dot(cross(ph, b), m) >= 0.0) hi = std::max(hi, pl);   // max on the arc
-    if (dot(cross(a, ph), m) <= 0.0 && dot(cross(ph, b), m) <= 0.0) lo = std::min(lo, -pl);  // -ph on the arc
-  }
-  if (in_p) hi = 1.0;
-  if (in_m) lo = -1.0;
-  constexpr double kWiden = 1e-4 + 1e-9;
-  return hi + kWiden > -(tau + 1e-5) && lo - kWiden < 2e-5;
-}
-
 void build_band_lists(BvhHost& out) {
   std::vector<V3> nh(out.n_prims);
   for (uint32_t k = 0; k < out.n_prims; ++k) {
@@ -363,43 +315,90 @@ void build_band_lists(BvhHost& out) {
   }
   const int kDirRes = (int)out.dir_res, kDirCells = 6 * kDirRes * kDirRes;
   // coarse-to-fine: a cell's candidates are its parent's entries whose band meets the cell's cap
-  // (the caps nest up to their 1e-4 rad widening, which cone_hits_band's caps all carry)
+  // (the caps nest up to their 1e-4 rad widening, which cone_hits_band's caps all carry), through
+  // resolutions 8, 64, then steps of 4 (or 2, 3) up to dir_res; the fine cells test their corners.
+  // Filtering keeps the candidates' order (ascending prim index).
   constexpr int kCoarse = 8;
-  const int kMid = std::min(kDirRes, 64), kSubMid = kMid / kCoarse, kSub = kDirRes / kMid;
+  std::vector<int> res{kCoarse};  // the filtering levels (each divides the next and dir_res)
+  if (kDirRes > 64) res.push_back(64);
+  while (res.back() * 2 < kDirRes) {
+    const int r = res.back();
+    const int s = kDirRes % (r * 4) == 0 && r * 4 < kDirRes ? 4 : kDirRes % (r * 2) == 0 ? 2 : kDirRes % (r * 3) == 0 ? 3 : 0;
+    if (s == 0) break;
+    res.push_back(r * s);
+  }
   out.band_off.assign(kDirCells + 1, 0);
-  std::vector<std::vector<uint32_t>> lists(kDirCells);
-  auto cone_of = [](int f, int res, int iu, int iv) {
-    return cell_cone(f, -1.0 + 2.0 * iu / res, -1.0 + 2.0 * (iu + 1) / res, -1.0 + 2.0 * iv / res,
-                     -1.0 + 2.0 * (iv + 1) / res);
+  auto cone_of = [](int f, int r, int iu, int iv) {
+    return cell_cone(f, -1.0 + 2.0 * iu / r, -1.0 + 2.0 * (iu + 1) / r, -1.0 + 2.0 * iv / r, -1.0 + 2.0 * (iv + 1) / r);
   };
-  // one task per coarse cell: its candidates, then its mid cells', then their fine cells'
+  // Each coarse cell's task appends its fine cells' lists to its own buffer (cell index and length in
+  // visiting order); the offsets and the global list are assembled after the tasks.
+  struct TaskOut {
+    std::vector<uint32_t> ents;
+    std::vector<std::pair<uint32_t, uint32_t>> cells;
+  };
+  constexpr int kTasks = 6 * kCoarse * kCoarse;
+  std::vector<TaskOut> outs(kTasks);
+  // cell (iu, iv) of face f at level lv (resolution res[lv]) with its candidates: its children's
+  // candidates by their caps, down to the fine cells' exact test
+  std::function<void(TaskOut&, int, size_t, int, int, const std::vector<uint32_t>&)> refine =
+      [&](TaskOut& o, int f, size_t lv, int iu, int iv, const std::vector<uint32_t>& cand) {
+        const int s = (lv + 1 < res.size() ? res[lv + 1] : kDirRes) / res[lv];
+        std::vector<uint32_t> sub;
+        if (lv + 1 == res.size()) {
+          // the children are fine cells: their corner directions, normalized once for the block
+          const int g = s + 1;
+          std::vector<V3> G((size_t)g * g);
+          for (int a = 0; a < g; ++a)
+            for (int b = 0; b < g; ++b) {
+              const V3 d = face_dir(f, -1.0 + 2.0 * (iu * s + a) / kDirRes, -1.0 + 2.0 * (iv * s + b) / kDirRes);
+              G[(size_t)a * g + b] = d * (1.0 / norm(d));
+            }
+          for (int su = 0; su < s; ++su) {
+            for (int sv = 0; sv < s; ++sv) {
+              const int ju = iu * s + su, jv = iv * s + sv;
+              const V3 c[4] = {G[(size_t)su * g + sv], G[(size_t)(su + 1) * g + sv], G[(size_t)(su + 1) * g + sv + 1],
+                               G[(size_t)su * g + sv + 1]};
+              // d.nhat over the cell: between its corners' values, widened by the edges' bulge -- on a
+              // great-circle arc of angle t between two corners, d is the chord point over its length
+              // (>= cos(t / 2)), so |d.nhat| exceeds the chord's linear value by at most 1 / cos(t / 2) - 1;
+              // the interior adds only +-1 when +-nhat is inside, far from the band for cells this small.
+              // Then the quad test's own widening of 1e-4 + 1e-9 (the kernel's dir_cell rounding).
+              double cmin = 1.0;
+              for (int i = 0; i < 4; ++i) cmin = std::min(cmin, dot(c[i], c[(i + 1) & 3]));
+              const double bulge = 1.0 / std::sqrt(std::max(0.5 * (1.0 + cmin), 1e-300)) - 1.0 + 1e-12;
+              const double wid = bulge + 1e-4 + 1e-9;
+              const size_t n0 = o.ents.size();
+              for (uint32_t k : cand) {
+                const V3 n = nh[k];
+                const double v0 = dot(c[0], n), v1 = dot(c[1], n), v2 = dot(c[2], n), v3 = dot(c[3], n);
+                const double hi = std::max(std::max(v0, v1), std::max(v2, v3)), lo = std::min(std::min(v0, v1), std::min(v2, v3));
+                if (hi + wid > -(out.band_tau + 1e-5) && lo - wid < 2e-5) o.ents.push_back(k);
+              }
+              o.cells.emplace_back((uint32_t)(((size_t)f * kDirRes + ju) * kDirRes + jv), (uint32_t)(o.ents.size() - n0));
+            }
+          }
+          return;
+        }
+        for (int su = 0; su < s; ++su) {
+          for (int sv = 0; sv < s; ++sv) {
+            const int ju = iu * s + su, jv = iv * s + sv;
+            const Cone c = cone_of(f, res[lv + 1], ju, jv);
+            sub.clear();
+            for (uint32_t k : cand)
+              if (cone_hits_band(c, nh[k], out.band_tau)) sub.push_back(k);
+            refine(o, f, lv + 1, ju, jv, sub);
+          }
+        }
+      };
   auto task = [&](int t) {
     const int f = t / (kCoarse * kCoarse), cu = (t / kCoarse) % kCoarse, cv = t % kCoarse;
     const Cone kc = cone_of(f, kCoarse, cu, cv);
-    std::vector<uint32_t> coarse, mid;
+    std::vector<uint32_t> coarse;
     for (uint32_t k = 0; k < out.n_prims; ++k)
       if (cone_hits_band(kc, nh[k], out.band_tau)) coarse.push_back(k);
-    for (int mu = 0; mu < kSubMid; ++mu) {
-      for (int mv = 0; mv < kSubMid; ++mv) {
-        const int ju = cu * kSubMid + mu, jv = cv * kSubMid + mv;
-        const Cone mc = cone_of(f, kMid, ju, jv);
-        mid.clear();
-        for (uint32_t k : coarse)
-          if (cone_hits_band(mc, nh[k], out.band_tau)) mid.push_back(k);
-        for (int su = 0; su < kSub; ++su) {
-          for (int sv = 0; sv < kSub; ++sv) {
-            const int iu = ju * kSub + su, iv = jv * kSub + sv;
-            const Quad fq = cell_quad(f, -1.0 + 2.0 * iu / kDirRes, -1.0 + 2.0 * (iu + 1) / kDirRes,
-                                      -1.0 + 2.0 * iv / kDirRes, -1.0 + 2.0 * (iv + 1) / kDirRes);
-            std::vector<uint32_t>& l = lists[((size_t)f * kDirRes + iu) * kDirRes + iv];
-            for (uint32_t k : mid)
-              if (quad_hits_band(fq, nh[k], out.band_tau)) l.push_back(k);
-          }
-        }
-      }
-    }
+    refine(outs[t], f, 0, cu, cv, coarse);
   };
-  constexpr int kTasks = 6 * kCoarse * kCoarse;
   const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   std::atomic<int> next{0};
   auto worker = [&]() {
@@ -409,10 +408,26 @@ void build_band_lists(BvhHost& out) {
   for (unsigned i = 1; i < nthreads && out.n_prims > 64; ++i) pool.emplace_back(worker);
   worker();
   for (auto& th : pool) th.join();
-  for (int c = 0; c < kDirCells; ++c) out.band_off[c + 1] = out.band_off[c] + (uint32_t)lists[c].size();
-  // entries: the prim index (hrt_bvh.h); the pre-check's normals, one per prim
+  for (const TaskOut& o : outs)
+    for (const auto& c : o.cells) out.band_off[c.first + 1] = c.second;
+  for (int c = 0; c < kDirCells; ++c) out.band_off[c + 1] += out.band_off[c];
   out.band_list.resize(out.band_off[kDirCells]);
-  for (int c = 0; c < kDirCells; ++c) std::copy(lists[c].begin(), lists[c].end(), out.band_list.begin() + out.band_off[c]);
+  next = 0;  // each task's lists to their places (disjoint ranges), on the same threads
+  auto copier = [&]() {
+    for (int t; (t = next.fetch_add(1)) < kTasks;) {
+      size_t at = 0;
+      for (const auto& c : outs[t].cells) {
+        std::copy(outs[t].ents.begin() + at, outs[t].ents.begin() + at + c.second, out.band_list.begin() + out.band_off[c.first]);
+        at += c.second;
+      }
+      std::vector<uint32_t>().swap(outs[t].ents);
+    }
+  };
+  pool.clear();
+  for (unsigned i = 1; i < nthreads && out.n_prims > 64; ++i) pool.emplace_back(copier);
+  copier();
+  for (auto& th : pool) th.join();
+  // (entries: the prim index, hrt_bvh.h) the pre-check's normals, one per prim
   out.band_nhat.assign((size_t)out.n_prims * 4, 0.0f);
   for (uint32_t k = 0; k < out.n_prims; ++k) {
     out.band_nhat[(size_t)k * 4] = (float)nh[k].x;
@@ -530,7 +545,7 @@ bool make_wq_nodes(const BvhHost& b, std::vector<float>& out, uint32_t width, ui
 }
 
 bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
-               uint32_t leaf_size, BvhHost& out, uint32_t wq_width, float band_tau) {
+               uint32_t leaf_size, BvhHost& out, uint32_t wq_width, float band_tau, bool bands) {
   out = BvhHost{};
   out.band_tau = band_tau;
   if (n_meshes > kBvhMaxMeshes) return false;
@@ -634,13 +649,61 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
     out.margin_frac = out.n_nodes ? msum / out.n_nodes : 0.0;
   }
   out.dir_res = (uint32_t)dir_res_for(out.n_prims);
-  build_band_lists(out);
+  if (bands) build_bands(out);
   // t-slack of the box test for a lane at distance <= R: abs = abs_coef R, rel
   const double e = 5.9604644775390625e-08, inv_tp = 1.02 / ((double)out.band_tau - out.rho_max - 4e-7);
   out.abs_coef = round_up(2.1 * (4.2 * e + out.rho_max) * inv_tp * (1.0 + 1e-6));
   out.rel_t = round_up((2.1 * (3.2 * e + out.rho_max) * inv_tp + 4 * e) * (1.0 + 1e-6));
   out.wq_ok = make_wq_nodes(out, out.wq_nodes, wq_width, &out.wq_n_nodes, &out.wq_width);
   return true;
+}
+
+// The lists are a function of the prim records (their order and normals), tau_g and dir_res alone, and
+// most of a scene's set-up time at 1024 cells per face edge (~0.5 s for island): the last two results
+// are kept for the process, so contexts of one scene (a rank group in one process, or a test suite's
+// many contexts) build them once.  A hit compares the whole prim image, not only its hash.
+struct BandCache {
+  std::vector<float> prims;
+  uint32_t dir_res = 0;
+  float tau = 0.0f;
+  std::vector<uint32_t> off, list;
+  std::vector<float> nhat;
+  float a1 = 0.0f;
+};
+
+void build_bands(BvhHost& out) {
+  static std::mutex mu;
+  static std::vector<std::shared_ptr<const BandCache>> kept;  // most recent last, at most 2
+  auto same = [&](const BandCache& c) {
+    return c.dir_res == out.dir_res && c.tau == out.band_tau && c.prims.size() == out.prims.size() &&
+           std::memcmp(c.prims.data(), out.prims.data(), out.prims.size() * sizeof(float)) == 0;
+  };
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    for (size_t i = kept.size(); i-- > 0;) {
+      if (!same(*kept[i])) continue;
+      const std::shared_ptr<const BandCache> c = kept[i];
+      kept.erase(kept.begin() + (long)i);
+      kept.push_back(c);
+      out.band_off = c->off;
+      out.band_list = c->list;
+      out.band_nhat = c->nhat;
+      out.band_a1 = c->a1;
+      return;
+    }
+  }
+  build_band_lists(out);
+  auto c = std::make_shared<BandCache>();
+  c->prims = out.prims;
+  c->dir_res = out.dir_res;
+  c->tau = out.band_tau;
+  c->off = out.band_off;
+  c->list = out.band_list;
+  c->nhat = out.band_nhat;
+  c->a1 = out.band_a1;
+  std::lock_guard<std::mutex> lock(mu);
+  kept.push_back(std::move(c));
+  if (kept.size() > 2) kept.erase(kept.begin());
 }
 
 }  // namespace hrt

@@ -85,8 +85,13 @@ constexpr float kBandTau = HRT_BAND_TAU;
 #ifndef HRT_DIR_RES_SMALL
 // r03z (tau 3e-3): 256 / 384 / 512 cells -- island 2.109 / 2.101 / 2.089 ms, FETCH_SIZE x2 0.32 / 0.76 /
 // 1.06 GB per frame; cave 5.945 / 5.871 / 5.827 ms, 0.40 / 0.64 / 0.80 GB: the finer lists are 1-2%
-// faster but no longer fit the L2 (island 512: 16.5 MB of entries + 6.3 MB of offsets), 256 kept.
-#define HRT_DIR_RES_SMALL 256
+// faster but no longer fit the L2 (island 512: 16.5 MB of entries + 6.3 MB of offsets), 256 kept then.
+// r05 (20-frame launches at bench.py's shape, profiles/r05/r05q-t_*): 256 / 512 / 1024 / 1536 / 2048
+// cells -- island 1.760 / 1.745 / 1.719 / 1.717 / 1.712 ms, cave 5.436 / 5.316 / 5.260 / 5.257 / 5.292 ms;
+// a bounce lane scans ~13 band entries per lookup at 256 on cave, 6.4 at 1024.  The time is worth more
+// than the L2 residency; 1024 (island 24 M entries + 25 MB of offsets, ~74 MB on the device; cave ~106
+// MB; tau_g 1.5e-3 / 2e-3 / 4e-3 / 5e-3 at 1024 were no better).
+#define HRT_DIR_RES_SMALL 1024
 #endif
 constexpr int kDirResMax = HRT_DIR_RES_SMALL;
 inline int dir_res_for(uint64_t entries) { return entries <= 8192 ? HRT_DIR_RES_SMALL : entries <= 32768 ? 128 : 64; }
@@ -123,8 +128,12 @@ bool make_wq_nodes(const BvhHost& b, std::vector<float>& out, uint32_t width, ui
 
 // Builds the hierarchy over every (mesh, triangle) entry of the scene.  Returns false (and leaves
 // `out` empty) when the scene has more than kBvhMaxMeshes meshes, kBvhMaxEntries entries or 2^26
-// triangles.
+// triangles.  bands = false leaves the grazing-band lists to a later build_bands (hrt_set_scene picks
+// the leaf size from the hierarchy first; the lists are most of the build's time).
 bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes, uint32_t n_meshes,
-               uint32_t leaf_size, BvhHost& out, uint32_t wq_width = kWqDefaultWidth, float band_tau = kBandTau);
+               uint32_t leaf_size, BvhHost& out, uint32_t wq_width = kWqDefaultWidth, float band_tau = kBandTau,
+               bool bands = true);
+// The grazing-band lists (band_off, band_list, band_nhat, band_a1) of a hierarchy built without them.
+void build_bands(BvhHost& out);
 
 }  // namespace hrt
