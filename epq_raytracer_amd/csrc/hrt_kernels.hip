@@ -2243,6 +2243,9 @@ __device__ __forceinline__ void sky_samples(const TileList& tl, bool active, f3 
 enum BounceMode { kBounceBrute = 0, kBounceCull = 1, kBounceBvh = 2, kBounceWq = 3, kBounceWqR = 4 };
 constexpr bool is_wq(int b) { return b == kBounceWq || b == kBounceWqR; }
 
+#ifndef HRT_PIXEL_POOL
+#define HRT_PIXEL_POOL 1
+#endif
 template <int Bounce, bool D, class CullSrc, class BvhSrc = BvhGlobal>
 __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t x, uint32_t lr, const CullSrc& csrc,
                                                   const BvhSrc& bsrc, uint32_t* list_lds, Coop& co,
@@ -2250,10 +2253,10 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   const Scene sc{P.rays, P.spheres, P.tris, P.meshes, P.tri_nhat};
   const hrt_push_constants& pc = P.pc;
   const GlobalTris src{reinterpret_cast<const float4*>(P.tris)};
-  const uint32_t y = global_row(lr, P);
+  uint32_t y = global_row(lr, P);
   uint32_t segs = 0, tests = 0;
   const bool active = x < pc.width && lr < kargs()->local_rows && y < pc.height;
-  const uint32_t id = active ? x + y * pc.width : 0u;
+  uint32_t id = active ? x + y * pc.width : 0u;
   const uint64_t tile_t0 = (D && P.tile_cycles) ? __builtin_readcyclecounter() : 0;
   f3 colour = mk(0.0f, 0.0f, 0.0f);
   uint32_t state = (pc.rng_offset + frame) * 719393u + id;  // raytracing.glsl:376, frame f of the launch
@@ -2304,6 +2307,16 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
   // after the other per lane -- a lane that finishes its pixel in one frame starts the pixel's next
   // frame (rng_offset + f, its own image) at once instead of idling until the wave's slowest lane ends.
   uint32_t fr = 0;
+  // Pixel pool (HRT_PIXEL_POOL, a whole tile's frame run with every lane active): the run's 64 x nrun
+  // pixel-frames are one pool, frame-major, and a lane that finishes a pixel-frame takes the pool's next
+  // one -- any pixel of the tile, not only its own pixel's next frame -- so the wave ends one pixel-frame
+  // after the pool empties instead of after its slowest pixel's nrun frames.  A pixel-frame's work is
+  // the same whichever lane runs it (its RNG seed, centre, samples in order, its own image), so every
+  // frame is unchanged.  A lane that takes another pixel reloads its ray centre (a line the item's
+  // start brought into the cache); fr = nrun once the pool is empty and the lane's last pixel-frame is
+  // stored.
+  const bool pool = HRT_PIXEL_POOL && nrun > 1u && __all(active);
+  uint32_t pool_next = 64u;  // (wave-uniform)
   if (HRT_SKY_LOOP && tl.ok && tl.n == 0u && pc.num_spheres == 0) {  // wave-uniform: every segment a miss
     const uint64_t s0 = (D && P.diag) ? __builtin_readcyclecounter() : 0;
     for (;; ++fr) {
@@ -2323,9 +2336,38 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     done = true;
   }
   while (__any(!done)) {
+    // (a loop: with num_samples <= 0 a new pixel-frame ends at once too, and each must still be stored)
+    while (pool) {
+      const bool need = !done && p.bounce > pc.max_bounces && sample >= pc.num_samples;
+      const unsigned long long nb = __ballot(need);
+      if (!nb) break;
+      {
+        if (need) store_pixel(P, x, lr, div3(colour, (float)pc.num_samples), frame + fr);
+        const uint32_t idx = pool_next + lanes_below(nb);
+        pool_next += (uint32_t)__popcll(nb);
+        if (need) {
+          if (idx < 64u * nrun) {
+            const uint32_t px = idx & 63u;
+            fr = idx >> 6;
+            x = (x & ~7u) + (px & 7u);
+            lr = (lr & ~7u) + (px >> 3);
+            y = global_row(lr, P);
+            id = x + y * pc.width;
+            const float4 rc = kargs()->rays[id];
+            centre = mk(rc.x, rc.y, rc.z);
+            colour = mk(0.0f, 0.0f, 0.0f);
+            sample = 0;
+            state = (pc.rng_offset + frame + fr) * 719393u + id;
+          } else {
+            done = true;
+            fr = nrun;
+          }
+        }
+      }
+    }
     if (!done && p.bounce > pc.max_bounces) {
       // (a while: with num_samples <= 0 every frame of the run ends at once and each must still be stored)
-      while (sample >= pc.num_samples && fr + 1u < nrun) {  // the pixel's next frame of the run
+      while (!pool && sample >= pc.num_samples && fr + 1u < nrun) {  // the pixel's next frame of the run
         store_pixel(P, x, lr, div3(colour, (float)pc.num_samples), frame + fr);
         ++fr;
         colour = mk(0.0f, 0.0f, 0.0f);
@@ -2414,7 +2456,7 @@ __device__ __forceinline__ void trace_fused_split(const TraceParams& P, uint32_t
     }
   }
   if (co.w != 0) return;  // cooperative tile: wave 0 of the group writes the results
-  if (active) {
+  if (active && fr < nrun) {
     colour = div3(colour, (float)pc.num_samples);
     store_pixel(P, x, lr, colour, frame + fr);
   }

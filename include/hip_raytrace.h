@@ -162,8 +162,9 @@ typedef struct hrt_stats {
   float total_trace_ms;   /* device time of all trace dispatches since reset */
   uint64_t wave_steps;    /* sum over work items of the item's longest per-lane segment count: lane
                              efficiency = segments / (64 * wave_steps).  A frame run of a multi-frame
-                             launch (hrt_compute_n) is one item: its lanes' segments summed over the run's
-                             frames, so the figure is comparable between launches of the same shape only */
+                             launch (hrt_compute_n) is one item: each lane's segments summed over the
+                             run's pixel-frames it took (any pixel of the tile), so the figure is
+                             comparable between launches of the same shape only */
   uint32_t last_kernel;   /* hrt_kernel the last trace ran (HRT_KERNEL_AUTO resolved) */
   uint32_t last_block;    /* its workgroup size (threads) */
   uint32_t last_frames;   /* frames the last trace launch held (hrt_compute_n packs up to

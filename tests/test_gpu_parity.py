@@ -855,12 +855,13 @@ def test_sky_items_bit_exact(what, variant):
                                                ("box", 7, 3), ("island", 9, 0), ("box", 7, 0), ("box", 9, -2)])
 def test_frame_runs_match_frame_loop(scene, variant, spp):
     """Frame runs (a persistent wave's grabbed items that are one tile's consecutive frames run as one
-    pass: each lane starts its pixel's next frame as soon as it finishes one) give the per-frame loop's
-    accumulator, last trace image and counters.  The debug library's HRT_DEBUG_OPT_GRAB_RUNS makes the
+    pass: the run's pixel-frames are one pool, and a lane that finishes one takes the pool's next -- any
+    pixel of the tile; HRT_PIXEL_POOL) give the per-frame loop's accumulator, last trace image and
+    counters.  The debug library's HRT_DEBUG_OPT_GRAB_RUNS makes the
     waves take 4 items per grab at this size (the product does so while many items remain).  spp <= 0
     (ADVICE r04): every frame of a run ends at once and each must still be stored.  wave_steps is not
-    compared: inside a run it is the largest per-lane segment sum over the run, not a sum of per-frame
-    maxima (hrt_stats.wave_steps)."""
+    compared: inside a run it is the largest per-lane segment sum over the pixel-frames each lane ran,
+    not a sum of per-frame maxima (hrt_stats.wave_steps)."""
     case = SceneCase(scene, (75, 41), spp, 8)
 
     def push(k):
