@@ -893,12 +893,15 @@ extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* 
   const uint32_t cap = (uint32_t)std::max<size_t>(
       1, std::min<size_t>(ctx->frames_per_launch, ((size_t)1 << 30) / std::max<size_t>(np * px_bytes, 1)));
   const bool batch = persistent_kernel(hrt::resolve_variant(p, ctx->variant)) && cap > 1 && n > 1;
-  if (batch && ctx->frame_stack_frames < std::min(cap, n)) {
+  // (sized for a whole launch of cap frames at once: a stack grown from a short first call -- bench.py's
+  // 5 warm-up frames -- was re-allocated by the next longer call, a device synchronisation and ~0.3 ms
+  // of hipFree / hipMalloc inside that call)
+  if (batch && ctx->frame_stack_frames < cap) {
     HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     free_dev(ctx, ctx->frame_stack);
     ctx->frame_stack_frames = 0;
-    HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->frame_stack, (size_t)std::min(cap, n) * np * px_bytes));
-    ctx->frame_stack_frames = std::min(cap, n);
+    HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->frame_stack, (size_t)cap * np * px_bytes));
+    ctx->frame_stack_frames = cap;
   }
   for (uint32_t done = 0; done < n;) {
     // near-equal launches: ceil(remaining / cap) of them
