@@ -1,6 +1,6 @@
 """Host-side cost of one bench step (bench.py's compute_n_then_render shape): the time from the step's
 start to hrt_compute_n's return, against the whole step (to the stream's end) and the trace launch's own
-HIP-event time.  python tools/host_overhead.py [--scene island] [--steps 20] [--reps 5]"""
+HIP-event time.  python tools/host_overhead.py [--scene island] [--steps 20] [--reps 5] [--warmup 5]"""
 import argparse
 import os
 import sys
@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--scene", default="island")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=5, help="frames of the warm-up hrt_compute_n")
     a = ap.parse_args()
     W, H = 1920, 1080
     camera, settings = E.preset(a.scene)
@@ -29,8 +30,8 @@ def main():
     raytrace.init()
     diffuse.next_frame(0, raytrace.image())
     frame = 1
-    ctx.compute_n(raytrace.push_constants(camera, frame, False), 5)
-    frame += 5
+    ctx.compute_n(raytrace.push_constants(camera, frame, False), a.warmup)
+    frame += a.warmup
     ctx.synchronize()
     for _ in range(a.reps):
         ctx.reset_stats()
