@@ -180,13 +180,17 @@ def dir_cell(d, res):
 
 def test_band_lists_cover_every_grazing_triangle(built):
     case, b = built
+    assert_band_coverage(b)
+
+
+def assert_band_coverage(b, n_dirs=6000):
     prims = b["prims"]
     if len(prims) == 0:
         return
     n = prims[:, 12:15].astype(np.float64)
     nh = n / np.linalg.norm(n, axis=1, keepdims=True)
     rng = np.random.default_rng(3)
-    d = rng.normal(size=(6000, 3))
+    d = rng.normal(size=(n_dirs, 3))
     # plus directions right at cube-face edges and corners, and exactly in some triangles' planes
     edge = np.array([[1, 1, 0.3], [1, -1, 0.2], [1, 1, 1], [-1, 1, -1], [0.5, 1, 1], [1, 0, 0], [0, 0, -1]], float)
     t = rng.integers(len(nh), size=300)
@@ -206,6 +210,24 @@ def test_band_lists_cover_every_grazing_triangle(built):
         have = set(band_idx[off[c]:off[c + 1]].tolist())
         missing = [k for k in need if k not in have]
         assert not missing, f"direction {d[i]} cell {c}: band prims {missing[:5]} missing"
+
+
+def test_band_lists_follow_the_scene_content():
+    """hrt_bvh.cpp build_bands keeps the last two list sets per process, keyed on the prim records, tau_g
+    and the cell count: a scene whose geometry changed (a rotated copy of island) gets its own lists,
+    which cover its grazing triangles; the first scene again gets the first lists back."""
+    case = SceneCase("island", (8, 8), 1, 1)
+    a = build(case.tris, case.meshes, leaf=2)
+    c, s_ = np.cos(0.4), np.sin(0.4)
+    R = np.array([[c, 0, s_], [0, 1, 0], [-s_, 0, c]], np.float64)
+    tris = case.tris.copy()
+    for f in ("a", "edge_one", "edge_two", "normal"):
+        tris[f][:, :3] = (tris[f][:, :3].astype(np.float64) @ R.T).astype(np.float32)
+    b = build(tris, case.meshes, leaf=2)
+    assert b["dir_res"] == a["dir_res"] and not np.array_equal(b["band"], a["band"])
+    assert_band_coverage(b, n_dirs=1500)
+    a2 = build(case.tris, case.meshes, leaf=2)
+    assert np.array_equal(a2["band"], a["band"]) and np.array_equal(a2["band_off"], a["band_off"])
 
 
 def test_band_entries_are_prim_indices(built):
