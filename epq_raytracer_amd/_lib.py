@@ -67,7 +67,7 @@ class Stats(ctypes.Structure):
                 ("reserved", c_uint32)]
 
 
-ABI_VERSION = 5  # HRT_ABI_VERSION this binding's signatures describe
+ABI_VERSION = 6  # HRT_ABI_VERSION this binding's signatures describe
 HRT_OK = 0
 STATUS_NAMES = {0: "HRT_OK", 1: "HRT_ERR_INVALID_ARGUMENT", 2: "HRT_ERR_NO_DEVICE", 3: "HRT_ERR_OUT_OF_MEMORY",
                 4: "HRT_ERR_NO_SCENE", 5: "HRT_ERR_HIP", 6: "HRT_ERR_IO", 7: "HRT_ERR_COMM"}
@@ -84,6 +84,7 @@ DEBUG_OPT_FAIL_ALLOC = 1001  # libhip_raytrace_debug.so only
 DEBUG_OPT_WQ_TRI_CAP = 1002  # libhip_raytrace_debug.so only
 DEBUG_OPT_GRAB_RUNS = 1003  # libhip_raytrace_debug.so only
 DEBUG_OPT_TIMELINE = 1004  # builds with -DHRT_TIMELINE=1 only (tools/timeline.py)
+DEBUG_OPT_STACK_LIMIT = 1005  # libhip_raytrace_debug.so only
 COMM_ID_BYTES = 128
 COMM_NONE, COMM_RCCL, COMM_RCCL_GROUP, COMM_DEVICE_COPY = 0, 1, 2, 3
 # hrt_kernel (include/hip_raytrace.h)
@@ -129,7 +130,7 @@ EXPORTED_SYMBOLS = (
     "hrt_get_diagnostics", "hrt_get_tile_profile", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
     "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory", "hrt_debug_math_check", "hrt_debug_math_check_rng", "hrt_debug_band_flatten", "hrt_debug_wq_protocol",
     "hrt_debug_timeline",
-    "hrt_stream", "hrt_last_error", "hrt_comm_unique_id", "hrt_comm_init", "hrt_comm_init_all", "hrt_comm_info",
+    "hrt_stream", "hrt_release_caches", "hrt_last_error", "hrt_comm_unique_id", "hrt_comm_init", "hrt_comm_init_all", "hrt_comm_info",
     "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
     "hrt_debug_bvh_build", "hrt_debug_bvh_wq_nodes",
     "hrt_obj_load", "hrt_obj_num_meshes", "hrt_obj_mesh", "hrt_obj_free",
@@ -208,6 +209,7 @@ def load(debug: bool = False) -> ctypes.CDLL:
         "hrt_set_option": (c_int32, [P, c_uint32, c_int64]),
         "hrt_stream": (c_void_p, [P]),
         "hrt_last_error": (c_char_p, [P]),
+        "hrt_release_caches": (c_int32, [P]),
         "hrt_host_create_rays": (c_uint32, [c_uint32, c_uint32, c_float, c_float, POINTER(c_float), P,
                                             POINTER(c_float)]),
         "hrt_host_view_matrix": (None, [POINTER(c_float), POINTER(c_float), POINTER(c_float)]),

@@ -810,7 +810,9 @@ hrt_status ensure_ring(hrt_context* ctx) {
 
 // The lane the next trace runs on (rotating over HRT_OPT_OVERLAP lanes, after the lane's last reader).
 hrt_status begin_lane(hrt_context* ctx, int* out) {
-  const int n = ctx->diag_on ? 1 : (int)std::max(1u, ctx->overlap);
+  // (diagnostics and the timeline record into one buffer per context: one lane, so no two launches
+  // interleave their records or reset each other's count -- ADVICE r05)
+  const int n = ctx->diag_on || ctx->timeline ? 1 : (int)std::max(1u, ctx->overlap);
   const int l = ctx->lane_used ? (ctx->cur_lane + 1) % n : 0;
   hrt::Lane& lane = ctx->lane[l];
   if (lane.free_set) HRT_HIP(ctx, hipStreamWaitEvent(lane.stream, lane.free, 0));
@@ -875,6 +877,14 @@ extern "C" hrt_status hrt_trace(hrt_context* ctx, const hrt_push_constants* pc) 
   return end_lane(ctx, l);
 }
 
+// The frame stack's allocation (the debug build can make it fail above HRT_DEBUG_OPT_STACK_LIMIT bytes).
+static hipError_t stack_alloc(hrt_context* ctx, void** p, size_t bytes) {
+#ifdef HRT_DEBUG_OPTIONS
+  if (ctx->debug_stack_limit > 0 && bytes > (size_t)ctx->debug_stack_limit) return hipErrorOutOfMemory;
+#endif
+  return hrt::dev_alloc(ctx, p, bytes);
+}
+
 extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* pc, uint32_t n) {
   if (!ctx || !pc) return HRT_ERR_INVALID_ARGUMENT;
   if (pc->init) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_compute_n: init dispatches go through hrt_trace");
@@ -892,20 +902,40 @@ extern "C" hrt_status hrt_compute_n(hrt_context* ctx, const hrt_push_constants* 
   // Frames per launch: up to HRT_OPT_FRAMES_PER_LAUNCH, and at most 1 GiB of frame images.
   const uint32_t cap = (uint32_t)std::max<size_t>(
       1, std::min<size_t>(ctx->frames_per_launch, ((size_t)1 << 30) / std::max<size_t>(np * px_bytes, 1)));
-  const bool batch = persistent_kernel(hrt::resolve_variant(p, ctx->variant)) && cap > 1 && n > 1;
-  // (sized for a whole launch of cap frames at once: a stack grown from a short first call -- bench.py's
-  // 5 warm-up frames -- was re-allocated by the next longer call, a device synchronisation and ~0.3 ms
-  // of hipFree / hipMalloc inside that call)
+  bool batch = persistent_kernel(hrt::resolve_variant(p, ctx->variant)) && cap > 1 && n > 1;
+  // The stack is sized for a whole launch of cap frames at once (a stack grown from a short first call --
+  // bench.py's 5 warm-up frames -- was re-allocated by the next longer call, a device synchronisation and
+  // ~0.3 ms of hipFree / hipMalloc inside that call).  Where that does not fit (several contexts on one
+  // device, little free memory) the call's own min(cap, n) frames are allocated instead; where even those
+  // do not fit, the call runs with the stack it has (more, shorter launches) or one launch per frame.
+  // Never an error: the frames are the same bytes whatever the launches hold.
   if (batch && ctx->frame_stack_frames < cap) {
-    HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    free_dev(ctx, ctx->frame_stack);
-    ctx->frame_stack_frames = 0;
-    HRT_HIP(ctx, hrt::dev_alloc(ctx, (void**)&ctx->frame_stack, (size_t)cap * np * px_bytes));
-    ctx->frame_stack_frames = cap;
+    const uint32_t need = std::min(cap, n);
+    void* fresh = nullptr;
+    uint32_t fresh_frames = 0;
+    auto try_alloc = [&](uint32_t frames) {
+      if (stack_alloc(ctx, &fresh, (size_t)frames * np * px_bytes) == hipSuccess) {
+        fresh_frames = frames;
+        return true;
+      }
+      (void)hipGetLastError();  // (a failed allocation is not a sticky error)
+      fresh = nullptr;
+      return false;
+    };
+    if (ctx->frame_stack_failed != cap && !try_alloc(cap)) ctx->frame_stack_failed = cap;
+    if (!fresh && ctx->frame_stack_frames < need) (void)try_alloc(need);
+    if (fresh) {
+      HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      free_dev(ctx, ctx->frame_stack);
+      ctx->frame_stack = fresh;
+      ctx->frame_stack_frames = fresh_frames;
+    }
   }
+  const uint32_t lcap = batch ? std::min(cap, ctx->frame_stack_frames) : 1;  // frames per launch this call
+  batch = batch && lcap > 1;
   for (uint32_t done = 0; done < n;) {
-    // near-equal launches: ceil(remaining / cap) of them
-    const uint32_t left = n - done, launches = batch ? (left + cap - 1) / cap : left;
+    // near-equal launches: ceil(remaining / lcap) of them
+    const uint32_t left = n - done, launches = batch ? (left + lcap - 1) / lcap : left;
     const uint32_t nf = (left + launches - 1) / launches;
     hrt::TraceParams q = p;
     q.pc.rng_offset = pc->rng_offset + done;  // u32, wrapping like the per-frame loop's pushes
@@ -1429,18 +1459,24 @@ extern "C" hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t val
       if (value < 0 || value > 1) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "grab runs must be 0 or 1");
       ctx->debug_grab_runs = (uint32_t)value;
       return HRT_OK;
+    case HRT_DEBUG_OPT_STACK_LIMIT:
+      if (value < 0) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "stack limit must be >= 0");
+      ctx->debug_stack_limit = value;
+      ctx->frame_stack_failed = 0;
+      return HRT_OK;
 #else
     case HRT_OPT_GRID_CUS:
     case HRT_DEBUG_OPT_FAIL_ALLOC:
     case HRT_DEBUG_OPT_WQ_TRI_CAP:
     case HRT_DEBUG_OPT_GRAB_RUNS:
+    case HRT_DEBUG_OPT_STACK_LIMIT:
       return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "debug option: only libhip_raytrace_debug.so accepts it");
 #endif
     case HRT_DEBUG_OPT_TIMELINE:
 #if HRT_TIMELINE
       if (value <= 0 || value > (1 << 24)) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "timeline capacity in [1, 2^24]");
       if (ctx->timeline) {
-        HRT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        HRT_HIP(ctx, hipDeviceSynchronize());  // (every lane's stream: a launch may still be recording)
         free_dev(ctx, ctx->timeline);
         free_dev(ctx, ctx->timeline_count);
       }
@@ -1475,6 +1511,12 @@ extern "C" hrt_status hrt_debug_timeline(hrt_context* ctx, uint64_t* out, uint32
 extern "C" void* hrt_stream(hrt_context* ctx) {
   if (!ctx || bind(ctx) != HRT_OK || hrt::flush_combines(ctx) != HRT_OK) return ctx ? (void*)ctx->stream : nullptr;
   return (void*)ctx->stream;
+}
+
+extern "C" hrt_status hrt_release_caches(uint64_t* freed_bytes) {
+  const uint64_t bytes = hrt::release_band_cache();
+  if (freed_bytes) *freed_bytes = bytes;
+  return HRT_OK;
 }
 
 extern "C" const char* hrt_last_error(const hrt_context* ctx) {

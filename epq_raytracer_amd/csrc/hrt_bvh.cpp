@@ -661,7 +661,9 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
 // The lists are a function of the prim records (their order and normals), tau_g and dir_res alone, and
 // most of a scene's set-up time at 1024 cells per face edge (~0.5 s for island): the last two results
 // are kept for the process, so contexts of one scene (a rank group in one process, or a test suite's
-// many contexts) build them once.  A hit compares the whole prim image, not only its hash.
+// many contexts) build them once.  A hit compares the whole prim image, not only its hash.  Resident
+// host cost: the prim image plus the lists, ~100 MB per entry for island and ~130 MB for cave at the
+// default resolution; hrt_release_caches() drops them.
 struct BandCache {
   std::vector<float> prims;
   uint32_t dir_res = 0;
@@ -671,9 +673,27 @@ struct BandCache {
   float a1 = 0.0f;
 };
 
+namespace {
+std::mutex band_cache_mu;
+std::vector<std::shared_ptr<const BandCache>> band_cache;  // most recent last, at most 2
+}  // namespace
+
+uint64_t release_band_cache() {
+  std::vector<std::shared_ptr<const BandCache>> gone;
+  {
+    std::lock_guard<std::mutex> lock(band_cache_mu);
+    gone.swap(band_cache);
+  }
+  uint64_t bytes = 0;
+  for (const auto& c : gone)
+    bytes += c->prims.size() * sizeof(float) + (c->off.size() + c->list.size()) * sizeof(uint32_t) +
+             c->nhat.size() * sizeof(float);
+  return bytes;  // (freed as `gone` goes out of scope; a build holding an entry keeps it alive until done)
+}
+
 void build_bands(BvhHost& out) {
-  static std::mutex mu;
-  static std::vector<std::shared_ptr<const BandCache>> kept;  // most recent last, at most 2
+  std::mutex& mu = band_cache_mu;
+  std::vector<std::shared_ptr<const BandCache>>& kept = band_cache;
   auto same = [&](const BandCache& c) {
     return c.dir_res == out.dir_res && c.tau == out.band_tau && c.prims.size() == out.prims.size() &&
            std::memcmp(c.prims.data(), out.prims.data(), out.prims.size() * sizeof(float)) == 0;

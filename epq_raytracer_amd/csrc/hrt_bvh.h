@@ -135,5 +135,7 @@ bool build_bvh(const hrt_triangle* tris, uint32_t n_tris, const hrt_mesh* meshes
                bool bands = true);
 // The grazing-band lists (band_off, band_list, band_nhat, band_a1) of a hierarchy built without them.
 void build_bands(BvhHost& out);
+// Drops the process-wide band-list cache of build_bands; returns the host bytes it held.
+uint64_t release_band_cache();
 
 }  // namespace hrt

@@ -134,12 +134,14 @@ struct hrt_context {
   uint32_t frames_per_launch = 64;  // HRT_OPT_FRAMES_PER_LAUNCH (hrt_compute_n)
   void* frame_stack = nullptr;      // hrt_compute_n: frame_stack_frames trace images
   uint32_t frame_stack_frames = 0;
+  uint32_t frame_stack_failed = 0;  // a whole-launch stack of this many frames did not fit: not retried
   uint32_t num_cus = 0;
   uint32_t bvh_leaf = 0;  // HRT_OPT_BVH_LEAF_SIZE for the next hrt_set_scene (0 = auto, hrt_bvh.h)
   uint32_t wq_node_radius = 0;  // HRT_OPT_WQ_NODE_RADIUS (0 = auto)
   uint32_t bvh_width = 4;  // HRT_OPT_BVH_WIDTH (hrt_bvh.h kWqDefaultWidth) for the next hrt_set_scene
   int64_t debug_fail_alloc = 0;   // debug build: fail the n-th device allocation of the next hrt_set_scene
   uint32_t debug_grab_runs = 0;   // debug build: HRT_DEBUG_OPT_GRAB_RUNS
+  int64_t debug_stack_limit = 0;  // debug build: HRT_DEBUG_OPT_STACK_LIMIT (frame-stack bytes that fit)
   uint32_t debug_wq_tri_cap = 0;  // debug build: HRT_DEBUG_OPT_WQ_TRI_CAP (triangle-pair stack capacity)
   unsigned long long* timeline = nullptr;  // HRT_TIMELINE builds: HRT_DEBUG_OPT_TIMELINE records (4 u64 each)
   uint32_t* timeline_count = nullptr;

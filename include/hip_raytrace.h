@@ -39,13 +39,14 @@
 extern "C" {
 #endif
 
-/* 5 (r05): HRT_DIAG_WQ_STEPS_* / WQ_MEMBERS (HRT_NUM_DIAG 29), HRT_DEBUG_OPT_TIMELINE + hrt_debug_timeline.
+/* 6 (r06): hrt_release_caches; HRT_DEBUG_OPT_STACK_LIMIT.
+ * 5 (r05): HRT_DIAG_WQ_STEPS_* / WQ_MEMBERS (HRT_NUM_DIAG 29), HRT_DEBUG_OPT_TIMELINE + hrt_debug_timeline.
  * 4 (r04): hrt_debug_wq_protocol; hrt_stats.last_frames; HRT_DIAG_SKY_* / PRIMARY_LANES / LOOP_ITERS /
  * LIVE_LANES (HRT_NUM_DIAG 24).
  * 3 (r03): hrt_debug_band_flatten.
  * 2 (r03): HRT_ERR_COMM, HRT_IMG_LOCAL, HRT_OPT_COMM_TIMEOUT_MS, collective error agreement;
  * hrt_debug_bvh_wq_nodes' width parameter; HRT_NUM_DIAG / HRT_NUM_SCENE_INFO grown (r02). */
-#define HRT_ABI_VERSION 5u
+#define HRT_ABI_VERSION 6u
 
 typedef enum hrt_status {
   HRT_OK = 0,
@@ -314,7 +315,11 @@ typedef enum hrt_option {
   /* builds with -DHRT_TIMELINE=1 only (tuning, tools/timeline.py): record, for each work item the persistent
    * kernels execute, its start / end time (s_memrealtime, 100 MHz), item word, frame, run length and
    * resident wave -- up to value records per launch (hrt_debug_timeline).  Other builds reject the key. */
-  HRT_DEBUG_OPT_TIMELINE = 1004
+  HRT_DEBUG_OPT_TIMELINE = 1004,
+  /* libhip_raytrace_debug.so only (tests): an hrt_compute_n frame-image allocation of more than value
+   * bytes fails as if the device were out of memory (0 = off), so the fallback from a whole launch's
+   * images to the call's own frames runs.  Results do not depend on it. */
+  HRT_DEBUG_OPT_STACK_LIMIT = 1005
 } hrt_option;
 
 /* Cull diagnostics of the bundle kernels (HRT_OPT_COUNTERS = 2), summed since the last reset. */
@@ -517,6 +522,13 @@ hrt_status hrt_set_option(hrt_context* ctx, uint32_t key, int64_t value);
 /* The context's HIP stream (hipStream_t), for callers that interoperate: work enqueued on it after
  * hrt_accumulate / hrt_compute_n follows them (a trace is joined by the combiner that reads it). */
 void* hrt_stream(hrt_context* ctx);
+
+/* Drops the library's process-wide host caches: the grazing-band lists of the last two scenes that
+ * hrt_set_scene built (shared by every context of one scene so that a rank group or a test suite builds
+ * them once; ~100 MB of host memory each for island, ~130 MB for cave).  Contexts keep working; the next
+ * hrt_set_scene of such a scene rebuilds its lists (~0.5 s).  *freed_bytes (may be NULL) receives the
+ * bytes released.  Thread-safe. */
+hrt_status hrt_release_caches(uint64_t* freed_bytes);
 
 /* Text of the last error on ctx (or of the last hrt_create failure when ctx is NULL). */
 const char* hrt_last_error(const hrt_context* ctx);

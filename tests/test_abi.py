@@ -33,7 +33,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_library_loads_and_reports_abi():
     lib = _lib.load()
-    assert lib.hrt_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.hrt_abi_version() == _lib.ABI_VERSION == 6
     assert lib.hrt_debug_build() == 0
     assert len(_lib.build_id()) == 16 and _lib.build_id() != "unknown"
 

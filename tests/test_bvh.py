@@ -230,6 +230,22 @@ def test_band_lists_follow_the_scene_content():
     assert np.array_equal(a2["band"], a["band"]) and np.array_equal(a2["band_off"], a["band_off"])
 
 
+def test_release_caches_drops_the_band_lists():
+    """hrt_release_caches: the process-wide band-list cache is released on request (its bytes
+    reported, nothing the second time), and a later build of the same scene rebuilds the same lists."""
+    lib = _lib.load()
+    case = SceneCase("island", (8, 8), 1, 1)
+    a = build(case.tris, case.meshes, leaf=2)
+    freed = ctypes.c_uint64(0)
+    assert lib.hrt_release_caches(ctypes.byref(freed)) == 0
+    # at least this scene's lists and prim image (cached once per process, whichever test built them)
+    assert freed.value >= (a["band"].size + a["band_off"].size) * 4
+    assert lib.hrt_release_caches(ctypes.byref(freed)) == 0 and freed.value == 0
+    assert lib.hrt_release_caches(None) == 0
+    b = build(case.tris, case.meshes, leaf=2)
+    assert np.array_equal(a["band"], b["band"]) and np.array_equal(a["band_off"], b["band_off"])
+
+
 def test_band_entries_are_prim_indices(built):
     """Band entries are prim indices (hrt_bvh.h "Grazing-band entries"): in range, no duplicates in a
     cell's list (the kernels upload them as 16-bit words up to 65536 prims)."""

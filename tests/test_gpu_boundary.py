@@ -516,6 +516,47 @@ def test_tile_lists_follow_camera_jitter_and_rays(overlap, split):
     assert np.array_equal(got, want), f"regenerated rays: {mismatch_report(got, want)}"
 
 
+@pytest.mark.parametrize("overlap", [1, 3])
+def test_probe_built_tile_lists_follow_the_camera(overlap):
+    """at 1,024 tiles or more the first trace of each lane is planned from a 1-sample probe,
+    which also builds the tile lists, and the main launch then skips its own list prepass.  256 x 256 (32 x
+    32 tiles) with overlap 3 probes on each of the first three traces, at alternating cameras; every
+    trace must equal a fresh context's with the probe off (lists built by the trace itself)."""
+    case = SceneCase("island", (256, 256), 2, 4)
+    s = case.settings
+    d0 = np.asarray(case.camera.direction, np.float32)
+    c, sn = np.float32(np.cos(0.5)), np.float32(np.sin(0.5))
+    d1 = np.float32([c * d0[0] + sn * d0[2], d0[1], -sn * d0[0] + c * d0[2]])
+    d2 = np.float32([c * d0[0] - sn * d0[2], d0[1] * 0.6, sn * d0[0] + c * d0[2]])
+    focal = s.camera_focal_length * 12.0
+
+    def push(k, direction):
+        pc = case.push(k)
+        pc.cam_alignment_mat[:] = [float(v) for v in E.view_matrix(direction, case.camera.up)]
+        return pc
+
+    def context(probe):
+        ctx = E.HrtContext(case.size, device=0)
+        ctx.set_option(_lib.OPT_PROBE, probe)
+        ctx.set_option(_lib.OPT_OVERLAP, overlap)
+        ctx.set_option(_lib.OPT_SPLIT, 1)
+        ctx.generate_rays(focal, s.viewport_height, s.up)
+        ctx.set_scene(None, case.spheres, case.tris, case.meshes)
+        return ctx
+
+    ctx = context(1)
+    for k, direction in enumerate([d2, d1, d2, d1, d0], start=1):
+        pc = push(k, direction)
+        ctx.trace(pc)
+        got = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+        ref = context(0)
+        ref.trace(pc)
+        want = ref.read(_lib.IMG_TRACE, _lib.FMT_RGBA8)
+        ref.close()
+        assert np.array_equal(got, want), f"frame {k}: {mismatch_report(got, want)}"
+    ctx.close()
+
+
 def test_camera_lists_after_a_variant_switch():
     """A kernel that neither builds nor reads the camera lists (LITERAL, BRUTE) leaves the lane's lists as
     they were: BUNDLE_WQ from position B, then LITERAL from A, then BUNDLE_WQ from A on the same lane must

@@ -435,6 +435,34 @@ def test_compute_n_arguments():
     ctx.close()
 
 
+@pytest.mark.parametrize("limit_frames, want_last", [(0, 4), (3, 2), (1, 1)])
+def test_compute_n_frame_stack_fallback(limit_frames, want_last):
+    """hrt_compute_n's whole-launch frame images (HRT_OPT_FRAMES_PER_LAUNCH of them) are an
+    allocation that may not fit.  When it fails (HRT_DEBUG_OPT_STACK_LIMIT makes every larger one fail)
+    the call allocates its own frames instead, or keeps the stack it has, or runs a launch per frame --
+    never an error, and byte for byte the per-frame loop.  limit 3: the 8-frame stack fails, the first
+    call's 3 frames fit, the second call's 4 do not (launches of 2 + 2 on the 3-frame stack); limit 1:
+    no stack at all."""
+    case = SceneCase("island", (64, 48), 2, 8)
+    loop = case.context()
+    for k in range(1, 8):
+        loop.trace(case.push(k))
+        loop.accumulate(k)
+    a = loop.stats()
+    want_acc, want_trace = loop.read(_lib.IMG_ACCUM), loop.read(_lib.IMG_TRACE)
+    loop.close()
+    ctx = case.context(debug=True, options={_lib.OPT_FRAMES_PER_LAUNCH: 8,
+                                            _lib.DEBUG_OPT_STACK_LIMIT: limit_frames * 64 * 48 * 4})
+    ctx.compute_n(case.push(1), 3)
+    ctx.compute_n(case.push(4), 4)
+    b = ctx.stats()
+    got_acc, got_trace = ctx.read(_lib.IMG_ACCUM), ctx.read(_lib.IMG_TRACE)
+    ctx.close()
+    assert b.last_frames == want_last
+    assert np.array_equal(got_trace, want_trace) and np.array_equal(got_acc, want_acc)
+    assert (b.segments, b.tri_tests, b.traces, b.accumulates) == (a.segments, a.tri_tests, a.traces, a.accumulates)
+
+
 @pytest.mark.parametrize("parts,tile", [(2, 16), (3, 16), (8, 4)])
 def test_row_tile_partition_reassembles_full_frame(parts, tile):
     from epq_raytracer_amd import rowtiles

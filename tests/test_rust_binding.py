@@ -1,6 +1,6 @@
-"""The Rust binding INTEGRATION.md publishes (the reference host's side of the drop-in: src/hrt_ffi.rs,
-replacing the Vulkano dispatch of /root/reference/src/raytrace_pipeline.rs:51-266 and
-src/diffuse.rs:35-136) against include/hip_raytrace.h, on the CPU.
+"""The Rust binding of the drop-in (src/hrt_ffi.rs, added by integration/epq_raytracer.patch, which
+replaces the Vulkano dispatch of /root/reference/src/raytrace_pipeline.rs:51-266 and
+src/diffuse.rs:35-136) and the excerpts INTEGRATION.md quotes, against include/hip_raytrace.h, on the CPU.
 
 There is no Rust toolchain in this image, so the binding is never compiled here.  This test is what
 keeps it from drifting from the ABI (the published `hrt_stats` was 56 B while the ABI-4
@@ -25,6 +25,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "hip_raytrace.h")
 DOC = os.path.join(ROOT, "INTEGRATION.md")
+PATCH = os.path.join(ROOT, "integration", "epq_raytracer.patch")
 
 # Rust scalar -> (canonical C type, size, align) on x86-64 / the reference's targets
 RUST_SCALARS = {
@@ -34,8 +35,10 @@ RUST_SCALARS = {
     "c_char": ("char", 1, 1), "c_void": ("void", 0, 1), "c_int": ("int32_t", 4, 4), "c_uint": ("uint32_t", 4, 4),
 }
 # the vulkano shader! records the binding passes verbatim (raytrace_shader::*) and the C records they are
-RUST_RECORDS = {"rs::Ray": "hrt_ray", "rs::Sphere": "hrt_sphere", "rs::Triangle": "hrt_triangle",
-                "rs::Mesh": "hrt_mesh", "rs::PushConstants": "hrt_push_constants"}
+# (src/hrt_ffi.rs defines them itself, in `mod records`, under the GLSL names)
+RECORD_NAMES = {"RayTracingMaterial": "hrt_material", "Ray": "hrt_ray", "Sphere": "hrt_sphere",
+                "Triangle": "hrt_triangle", "Mesh": "hrt_mesh", "PushConstants": "hrt_push_constants"}
+RUST_RECORDS = {"rs::" + k: v for k, v in RECORD_NAMES.items()}
 # C spellings -> canonical
 C_ALIASES = {"int": "int32_t", "unsigned": "uint32_t", "hrt_status": "int32_t", "long long": "int64_t"}
 
@@ -52,6 +55,34 @@ def _rust_blocks(text):
 def _rust_source(text=None):
     text = open(DOC).read() if text is None else text
     src = "\n".join(_rust_blocks(text))
+    return re.sub(r"//[^\n]*", "", src)
+
+
+def patch_files(patch_text):
+    """path -> (removed lines, added lines) of every file a unified diff touches."""
+    out, cur = {}, None
+    for line in patch_text.splitlines():
+        if line.startswith("+++ "):
+            cur = line[4:].split("\t")[0].split("/", 1)[1]
+            out[cur] = ([], [])
+        elif line.startswith("--- ") or line.startswith("diff ") or line.startswith("@@"):
+            continue
+        elif cur and line.startswith("+"):
+            out[cur][1].append(line[1:])
+        elif cur and line.startswith("-"):
+            out[cur][0].append(line[1:])
+    return out
+
+
+def ffi_text(patch_text=None):
+    """src/hrt_ffi.rs as the patch adds it (a new file: its added lines are the whole file)."""
+    patch_text = open(PATCH).read() if patch_text is None else patch_text
+    removed, added = patch_files(patch_text)["src/hrt_ffi.rs"]
+    assert not removed
+    return "\n".join(added) + "\n"
+
+
+def _strip_rust_comments(src):
     return re.sub(r"//[^\n]*", "", src)
 
 
@@ -124,6 +155,8 @@ def rust_canon(ty):
         return ("scalar", RUST_SCALARS[ty][0])
     if ty in RUST_RECORDS:
         return ("record", RUST_RECORDS[ty])
+    if ty in RECORD_NAMES:
+        return ("record", RECORD_NAMES[ty])
     if re.match(r"hrt_\w+$", ty):
         return ("record", ty)
     raise AssertionError(f"unknown Rust FFI type {ty!r}")
@@ -142,7 +175,7 @@ def rust_layout(fields, structs):
             m = re.match(r"\[(.*);\s*(\d+)\]$", ty.strip())
             s, a = size_align(m.group(1))
             return s * int(m.group(2)), a
-        name = next((k for k, v in structs.items() if k == c[1]), None)
+        name = next((k for k in structs if RECORD_NAMES.get(k, k) == c[1]), None)
         assert name, f"record {c[1]} has no #[repr(C)] declaration in the binding"
         s, a, _ = rust_layout(structs[name], structs)
         return s, a
@@ -270,29 +303,43 @@ def c_layout(structs, names):
 
 # ---- checks --------------------------------------------------------------------------------------
 
-def check_binding(text):
-    """Every mismatch between the binding in `text` and the header, as strings."""
+def _flat_array(c):
+    """('array', elem, n) nests -> (scalar elem, total element count); anything else unchanged."""
+    n = 1
+    while c[0] == "array":
+        n *= c[2]
+        c = c[1]
+    return c, n
+
+
+def check_binding(text, rust=False, complete=True):
+    """Every mismatch between the binding in `text` (INTEGRATION.md's ```rust blocks, or Rust source
+    when rust=True) and the header, as strings.  complete: every public header function must be
+    declared (the binding itself; INTEGRATION.md only quotes excerpts)."""
     errs = []
-    rsrc, csrc = _rust_source(text), c_source()
+    rsrc, csrc = (_strip_rust_comments(text) if rust else _rust_source(text)), c_source()
     rs, cs = rust_structs(rsrc), c_structs(csrc)
-    layouts = c_layout(cs, [n for n in rs if n in cs])
+    cname = {n: RECORD_NAMES.get(n, n) for n in rs}
+    layouts = c_layout(cs, sorted({cname[n] for n in rs if cname[n] in cs}))
     for name, fields in rs.items():
-        if name not in cs:
+        if cname[name] not in cs:
             errs.append(f"struct {name}: not in the header")
             continue
-        cf = cs[name]
+        cf = cs[cname[name]]
         if [f for f, _ in fields] != [f for f, _, _ in cf]:
             errs.append(f"struct {name}: fields {[f for f, _ in fields]} != header {[f for f, _, _ in cf]}")
             continue
         for (fn, rty), (_, cty, n) in zip(fields, cf):
-            want = ("array", c_canon_type(cty), None) if n else c_canon_type(cty)
             got = rust_canon(rty)
-            if n:
-                got = ("array", got[1], None) if got[0] == "array" else got
+            if n:  # C `T x[n]` against Rust [T; n] (or nested arrays of the same element count)
+                want = (c_canon_type(cty), int(n))
+                got = _flat_array(got) if got[0] == "array" else (got, None)
+            else:
+                want = c_canon_type(cty)
             if got != want:
                 errs.append(f"struct {name}.{fn}: Rust {rty} != C {cty}{'[' + n + ']' if n else ''}")
         size, _, offs = rust_layout(fields, rs)
-        csize, coffs = layouts[name]
+        csize, coffs = layouts[cname[name]]
         if size != csize:
             errs.append(f"struct {name}: Rust repr(C) size {size} != C sizeof {csize}")
         for (fn, _), o in zip(fields, offs):
@@ -315,7 +362,7 @@ def check_binding(text):
         if rret != cret:
             errs.append(f"fn {name}: returns Rust {ret} != C {cret}")
     public = {n for n in cfn if not n.startswith("hrt_debug_") or n == "hrt_debug_build"}
-    for name in sorted(public - set(rfn)):
+    for name in sorted(public - set(rfn) if complete else ()):
         errs.append(f"fn {name}: in the header, missing from the binding")
     vals = c_values(csrc)
     for name, v in rust_consts(rsrc).items():
@@ -327,24 +374,39 @@ def check_binding(text):
 
 
 def test_binding_matches_header():
-    errs = check_binding(open(DOC).read())
+    errs = check_binding(ffi_text(), rust=True)
+    assert not errs, "\n".join(errs)
+
+
+def test_integration_excerpts_match_header():
+    errs = check_binding(open(DOC).read(), complete=False)
     assert not errs, "\n".join(errs)
 
 
 def test_binding_declares_the_abi_records():
-    rs = rust_structs(_rust_source())
-    assert {"hrt_create_info", "hrt_stats", "hrt_layout"} <= set(rs)
+    rs = rust_structs(_strip_rust_comments(ffi_text()))
+    assert {"hrt_create_info", "hrt_stats", "hrt_layout"} | set(RECORD_NAMES) <= set(rs)
     size, align, _ = rust_layout(rs["hrt_stats"], rs)
     assert (size, align) == (64, 8)
+    size, align, offs = rust_layout(rs["PushConstants"], rs)
+    assert (size, align, offs[2], offs[-1]) == (124, 4, 80, 120)
 
 
 def test_checker_catches_the_r04_drift():
     """The r04 text: hrt_stats without ABI 4's last_frames / reserved (56 B against 64 B)."""
-    text = open(DOC).read()
-    old = re.sub(r",\s*pub last_frames: u32,\s*pub reserved: u32", "", text)
+    text = ffi_text()
+    old = re.sub(r"\n\s*pub last_frames: u32,\n\s*pub reserved: u32,", "", text)
     assert old != text
-    errs = check_binding(old)
+    errs = check_binding(old, rust=True)
     assert any("struct hrt_stats" in e for e in errs), errs
+
+
+def _swap_lines(text, a, b):
+    lines = text.split("\n")
+    i = next(k for k, ln in enumerate(lines) if ln.strip() == a)
+    j = next(k for k, ln in enumerate(lines) if ln.strip() == b)
+    lines[i], lines[j] = lines[j], lines[i]
+    return "\n".join(lines)
 
 
 @pytest.mark.parametrize("edit, what", [
@@ -353,13 +415,19 @@ def test_checker_catches_the_r04_drift():
     (lambda t: re.sub(r"HRT_ABI_VERSION: u32 = (\d+);", lambda m: f"HRT_ABI_VERSION: u32 = {int(m.group(1)) + 1};", t),
      "HRT_ABI_VERSION"),
     (lambda t: t.replace("bytes: usize) -> i32;", "bytes: u32) -> i32;", 1), "fn hrt_read_image"),
-    (lambda t: t.replace("pub fn hrt_reset_stats(ctx: *mut hrt_context) -> i32;\n", ""), "hrt_reset_stats"),
+    (lambda t: t.replace("    pub fn hrt_reset_stats(ctx: *mut hrt_context) -> i32;\n", ""), "hrt_reset_stats"),
+    # a shifted push-block field (the block of src/raytrace_pipeline.rs:243-257 packed into the wrong slot)
+    (lambda t: _swap_lines(t, "pub num_samples: i32,", "pub jitter_size: f32,"), "struct PushConstants"),
+    (lambda t: t.replace("pub cam_alignment_mat: [[f32; 4]; 4],", "pub cam_alignment_mat: [[f32; 4]; 3],"),
+     "struct PushConstants"),
+    (lambda t: _swap_lines(t, "pub first_index: u32,", "pub len: u32,"), "struct Mesh"),
+    (lambda t: t.replace("pub centre: [f32; 3],", "pub centre: [f32; 4],"), "struct Sphere"),
 ])
 def test_checker_catches_edits(edit, what):
-    text = open(DOC).read()
+    text = ffi_text()
     changed = edit(text)
     assert changed != text, what
-    errs = check_binding(changed)
+    errs = check_binding(changed, rust=True)
     assert any(what in e for e in errs), errs
 
 
