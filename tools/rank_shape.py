@@ -6,7 +6,9 @@ line states each partition's kernel time against (whole-frame kernel time / N).
 
     python tools/rank_shape.py [--gpus 8] [--scene island] [--rounds 2] [--warmup 5] [--steps 20]
 
-Prints one JSON line per (round, partition) and a summary line: slowest / (whole / N).
+Prints one JSON line per (round, partition) and a summary line: per round, the slowest partition against
+that round's whole frame / N (an N-GPU step waits for its slowest rank in that run); the summary's
+slowest_over_fair is the worst round.
 """
 import argparse
 import json
@@ -74,15 +76,21 @@ def main():
             per[p].append(k)
             print(json.dumps({"round": r, "part": p, "kernel_ms": round(k, 4), "wall_ms": round(w, 4),
                               "segments": s}), flush=True)
-    fair = min(whole) / a.gpus
-    best = {p: min(v) for p, v in per.items()}
-    slow = max(best, key=best.get)
+    # An N-GPU step waits for its slowest rank IN THAT RUN: per round, the slowest
+    # part against that round's whole frame / N; the summary is the worst round, not each part's best.
+    runs = []
+    for r in range(a.rounds):
+        fair_r = whole[r] / a.gpus
+        slow_r = max(parts, key=lambda p: per[p][r])
+        runs.append({"round": r, "fair_share_ms": round(fair_r, 4), "slowest_part": slow_r,
+                     "slowest_ms": round(per[slow_r][r], 4), "slowest_over_fair": round(per[slow_r][r] / fair_r, 4)})
+    worst = max(runs, key=lambda x: x["slowest_over_fair"])
     print(json.dumps({"summary": True, "scene": a.scene, "gpus": a.gpus, "shape": f"{a.warmup} warm-up + {a.steps}",
-                      "whole_kernel_ms": round(min(whole), 4), "fair_share_ms": round(fair, 4),
-                      "part_kernel_ms": {p: round(v, 4) for p, v in best.items()},
-                      "slowest_part": slow, "slowest_over_fair": round(best[slow] / fair, 4),
+                      "whole_kernel_ms": [round(v, 4) for v in whole],
+                      "part_kernel_ms": {p: [round(v, 4) for v in per[p]] for p in parts},
+                      "runs": runs, "slowest_over_fair": worst["slowest_over_fair"],
+                      "basis": "per run: max over parts / (that run's whole frame / N); summary = worst run",
                       "options": a.option}), flush=True)
-
 
 if __name__ == "__main__":
     main()
