@@ -220,16 +220,28 @@ def main():
     frame = 1
 
     lib_gather = dist_on and not gloo
+    lib_comm_error = None
     if lib_gather:  # RCCL communicator inside the library: rank 0's id shared through torch.distributed
         ctx.set_option(_lib.OPT_COMM_TIMEOUT_MS, args.comm_timeout_ms)
         uid = [E.HrtContext.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
+        failed = 0
         try:
             ctx.comm_init(uid[0], rank, world)
         except _lib.HrtError as e:  # (the library's error text; every rank fails, none waits past the timeout)
-            print(f"bench.py rank {rank}/{world}: {e}", file=sys.stderr, flush=True)
-            os._exit(3)
-    local = torch.empty((ctx.local_rows, W, 4), dtype=torch.uint8, device=coll_dev) if dist_on and gloo else None
+            print(f"bench.py rank {rank}/{world}: library communicator: {e}", file=sys.stderr, flush=True)
+            lib_comm_error = str(e)
+            failed = 1
+        # (decided together: if any rank has no library communicator, no rank enters its gather)
+        flag = torch.tensor([failed], dtype=torch.int32, device=coll_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if int(flag[0]):
+            # the frame is still gathered, by torch.distributed's own all-gather of the same row blocks
+            # (RCCL through torch), and the line says so -- a scaling curve with the reason beside it
+            lib_gather = False
+            lib_comm_error = lib_comm_error or "another rank's hrt_comm_init failed"
+    torch_gather = dist_on and not lib_gather  # the gloo rehearsal, or the fallback above
+    local = torch.empty((ctx.local_rows, W, 4), dtype=torch.uint8, device=coll_dev) if torch_gather else None
     full = torch.empty((H, W, 4), dtype=torch.uint8, device=f"cuda:{device}") if lib_gather and rank == 0 else None
 
     def present():
@@ -363,7 +375,9 @@ def main():
                        "launch_frames": int(st.last_frames),  # the timed launches' frames, as the library split them
                        "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                        "parallelism": (f"row-tiles{world}x{args.row_tile} (" +
-                                       ("RCCL ncclGather behind hrt_read_image" if lib_gather else "gloo all-gather")
+                                       ("RCCL ncclGather behind hrt_read_image" if lib_gather else
+                                        "gloo all-gather" if gloo else
+                                        "torch.distributed all-gather: the library's communicator failed")
                                        + ")" if dist_on else "single-gpu"),
                        "launcher": ("bench.py --gpus (own rank processes)" if os.environ.get("BENCH_SPAWNED")
                                     else "torch.distributed.run" if dist_on else "single process"),
@@ -400,6 +414,8 @@ def main():
                                                                        last_trace)
         if ranks is not None:
             line["ranks"] = ranks
+        if lib_comm_error is not None:
+            line["lib_comm_error"] = lib_comm_error
         if dist_on and args.verify:
             line["gather_check"] = verify_gather(args, gathered, settings, camera, device, last_frame)
         print(json.dumps(line), flush=True)

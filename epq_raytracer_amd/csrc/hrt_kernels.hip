@@ -1517,6 +1517,9 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
 #ifndef HRT_WQ_BAND_EARLY
 #define HRT_WQ_BAND_EARLY 0  // (r05b: neutral, island 1.786 / 1.787, cave 5.405 / 5.400 ms) a bounce lane's direction-cell offsets requested at the batch's start (r05)
 #endif
+#ifndef HRT_WQ_BAND_AHEAD
+#define HRT_WQ_BAND_AHEAD 1  // band-list rounds whose entry loads are in flight at once (1: one round ahead)
+#endif
 #ifndef HRT_WQ_TRI_MIN
 #define HRT_WQ_TRI_MIN 64u  // a triangle step runs once this many triangle pairs wait (or no node pair is left)
 #endif
@@ -1905,6 +1908,31 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
     // round's normal load and before its check, so a round waits for the (cache-resident) normal
     // alone while the next round's (mostly L2-missing) entry load is in flight.  (The last round
     // fetches a round past the end too: a conditional load would make the normal's wait a full drain.)
+#if HRT_WQ_BAND_AHEAD > 1
+    // (A/B) the entry loads of the first HRT_WQ_BAND_AHEAD rounds issued together, then each round
+    // fetches the round that far ahead: the lists' random lines (a 74 MB structure no L2 holds) wait
+    // in parallel instead of one round at a time
+    uint32_t own_r[HRT_WQ_BAND_AHEAD], q_r[HRT_WQ_BAND_AHEAD];
+#pragma unroll
+    for (int i = 0; i < HRT_WQ_BAND_AHEAD; ++i) {
+      own_r[i] = 0u;
+      q_r[i] = 0u;
+      if (total > 64u * (uint32_t)i) fetch(64u * (uint32_t)i, own_r[i], q_r[i]);
+    }
+    for (uint32_t base = 0; base < total; base += 64u) {
+      if (tc + 64u > tcap) tri_step64();  // room for this round's pairs
+      const uint32_t own = own_r[0], q = q_r[0];
+      const float4 nh = nhat[q];
+#pragma unroll
+      for (int i = 0; i + 1 < HRT_WQ_BAND_AHEAD; ++i) {
+        own_r[i] = own_r[i + 1];
+        q_r[i] = q_r[i + 1];
+      }
+      uint32_t own_n, q_n;
+      fetch(base + 64u * HRT_WQ_BAND_AHEAD, own_n, q_n);
+      own_r[HRT_WQ_BAND_AHEAD - 1] = own_n;
+      q_r[HRT_WQ_BAND_AHEAD - 1] = q_n;
+#else
     uint32_t own = 0, q = 0;
     if (total) fetch(0u, own, q);
     for (uint32_t base = 0; base < total; base += 64u) {
@@ -1912,6 +1940,7 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
       const float4 nh = nhat[q];
       uint32_t own_n, q_n;
       fetch(base + 64u, own_n, q_n);
+#endif
       BandCheck oc = bc;
       oc.d = shfl3(bc.d, own);
 #if HRT_WQ_BAND_PLANE
@@ -1931,8 +1960,10 @@ __device__ __forceinline__ void world_hit_bounce_wq(const Scene& sc, const Trace
 #endif
       tc += (uint32_t)__popcll(pb);
       band_tests += push ? 1u : 0u;
+#if HRT_WQ_BAND_AHEAD <= 1
       own = own_n;
       q = q_n;
+#endif
     }
   }
   // pair traversal: the root is tested per lane, then (ray, node group) / (ray, triangle) pairs
