@@ -208,6 +208,7 @@ void free_scene(hrt_context* ctx, SceneBufs& s, bool keep_rays) {
   free_dev(ctx, s.bvh_band_off);
   free_dev(ctx, s.bvh_band);
   free_dev(ctx, s.bvh_band_nhat);
+  free_dev(ctx, s.bvh_band_rec);
   free_dev(ctx, s.bvh_entries);
   free_dev(ctx, s.bvh_keybase);
   for (int l = 0; l < kLanes; ++l) {
@@ -537,6 +538,16 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
         (st = up(s.bvh_entries, bvh.entries, "bvh entries")) != HRT_OK ||
         (st = up(s.bvh_keybase, bvh.key_base, "bvh key bases")) != HRT_OK)
       return st;
+    // BUNDLE_WQ's per-cell band records (hrt_kernels.hip band_cell), built on the device from the lists
+    // just uploaded: one 32 B record per direction cell (6 x 1,024^2 cells: 201 MB), 16-bit lists only
+    const size_t cells = bvh.band_off.empty() ? 0 : bvh.band_off.size() - 1;
+    if (!bvh.band_wide() && cells) {
+      hipError_t e = alloc((void**)&s.bvh_band_rec, cells * 32);
+      if (e == hipSuccess)
+        e = hrt::launch_band_records(s.bvh_band_off, static_cast<const uint32_t*>(s.bvh_band), s.bvh_band_rec,
+                                     (uint32_t)cells, ctx->stream);
+      if (e != hipSuccess) return hip_fail(ctx, e, "hrt_set_scene: band records");
+    }
   }
   s.bvh_info[HRT_SCENE_BVH_NODES] = bvh.n_nodes;
   s.bvh_info[HRT_SCENE_BVH_PRIMS] = bvh.n_prims;
@@ -676,6 +687,7 @@ hrt::TraceParams make_params(hrt_context* ctx, const hrt_push_constants* pc, int
   p.bvh_sah_milli = s.bvh_info[HRT_SCENE_BVH_SAH_MILLI];
   p.bvh_band = s.bvh_band;
   p.bvh_band_nhat = s.bvh_band_nhat;
+  p.bvh_band_rec = s.bvh_band_rec;
   p.bvh_band_wide = s.bvh_band_wide;
   p.bvh_band_bits = s.bvh_band_bits;
   p.bvh_entries = s.bvh_entries;

@@ -60,6 +60,7 @@ struct TraceParams {
   uint32_t bvh_sah_milli;        // hierarchy quality (HRT_SCENE_BVH_SAH_MILLI)
   const void* bvh_band;          // grazing-band entries: prim indices, 16-bit (32-bit when bvh_band_wide)
   const float4* bvh_band_nhat;   // per prim: its unit normal (the entries' pre-check)
+  const uint32_t* bvh_band_rec;  // BUNDLE_WQ: 8 dwords per direction cell (start, length, 12 first entries), or null
   uint32_t bvh_band_wide;
   uint32_t bvh_band_bits;        // bit width of the longest band list
   uint32_t cam_lists_ready;      // (host) cam_tris / cam_cull / cam_meta already hold this camera's lists
@@ -104,6 +105,9 @@ hipError_t launch_clear(uint32_t* img8, float4* img32, size_t npix, hipStream_t 
 hipError_t launch_accumulate_frames(uint32_t* cur8, const uint32_t* stack8, float4* cur32, const float4* stack32,
                                    size_t npix, uint32_t nf, uint32_t frame0, hipStream_t stream);
 hipError_t launch_tri_normals(const hrt_triangle* tris, float4* nhat, uint32_t n, hipStream_t stream);
+// BUNDLE_WQ's per-cell band records from the offsets and the 16-bit lists (hrt_kernels.hip band_cell).
+hipError_t launch_band_records(const uint32_t* off, const uint32_t* band16, uint32_t* rec, uint32_t cells,
+                               hipStream_t stream);
 hipError_t launch_accumulate(uint32_t* cur8, const uint32_t* new8, float4* cur32, const float4* new32, size_t npix,
                              uint32_t frame, hipStream_t stream);
 // Row-tile framebuffer assembly: gathered = parts x local_rows rows (rank-major), frame = height rows of
