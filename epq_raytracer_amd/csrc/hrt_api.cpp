@@ -326,7 +326,7 @@ extern "C" hrt_status hrt_create(const hrt_create_info* info, hrt_context** out_
     else
       e = hrt::dev_alloc(ctx, (void**)&l.trace32, np * 16);
     if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(trace)"));
-    if ((e = hrt::dev_alloc(ctx, (void**)&l.sched, 256 * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(sched)"));
+    if ((e = hrt::dev_alloc(ctx, (void**)&l.sched, hrt::kSchedWords * 4)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(sched)"));
     if ((e = hrt::dev_alloc(ctx, (void**)&l.tile_cost, tiles * 4)) != hipSuccess)
       return bail(hip_fail(ctx, e, "hipMalloc(tile costs)"));
     if ((e = hrt::dev_alloc(ctx, (void**)&l.item_buf, tiles * 64 * 4)) != hipSuccess)

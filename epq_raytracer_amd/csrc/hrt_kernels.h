@@ -8,6 +8,8 @@
 
 namespace hrt {
 
+constexpr uint32_t kSchedWords = 1024;  // TraceParams::sched (hrt_kernels.hip kSchedHist ...)
+
 // Kernel argument block (passed by value; lives in the kernarg segment, read through SGPRs).
 struct TraceParams {
   const float4* rays;            // W*H sample centres, indexed by global pixel id
@@ -33,7 +35,7 @@ struct TraceParams {
   uint32_t sec_batch;            // bounce segments run once this many lanes of a wave wait (1..64)
   // Persistent (LDS) variants' scheduler: sched[0] work counter, [1] item count, [2] heavy tiles,
   // [3] first heavy cost bucket, [5] cooperative-item counter, [6..7] u64 sum of tile costs,
-  // [8..199] planner histogram / offsets / cursors (256 words); tile_cost per 8x8 tile (shader clocks / 16, this trace);
+  // [8..) planner histogram / offsets / cursors (kSchedWords in all); tile_cost per 8x8 tile (shader clocks / 16, this trace);
   // item_buf (tiles x 8) the planned items; items = item_buf when this trace follows a plan.
   uint32_t* sched;
   uint32_t* tile_cost;

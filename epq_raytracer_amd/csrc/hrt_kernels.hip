@@ -2796,13 +2796,22 @@ __device__ __forceinline__ void tile_loop(const TraceParams& P, unsigned long lo
 // factor x (sum of costs / resident waves), to the bucket, i.e. a tile that alone would take `factor`
 // times a wave's fair share of the frame; each runs as 2, 4 or 8 items (bucket_items, <= split_k).  sched[8..71] histogram, [72..135] bucket offsets,
 // [136..199] bucket cursors, [3] first heavy bucket.
-constexpr uint32_t kPlanBuckets = 64;
+#ifndef HRT_PLAN_SUB
+// log2 of the planner's cost buckets per octave: eighth-octave buckets put a rank's long items nearer to
+// their exact longest-first order (r06p: the slowest of ranks 3 and 6 -1.7% per run on island, -1.1% on
+// cave; half-octave buckets left tiles up to 1.41x apart in arbitrary order)
+#define HRT_PLAN_SUB 3
+#endif
+constexpr uint32_t kPlanSub = HRT_PLAN_SUB, kPlanBuckets = 32u << kPlanSub;
 __device__ __forceinline__ uint32_t cost_bucket(unsigned long long c) {
-  if (c < 2) return 0;
+  if (c < (2u << kPlanSub)) return (uint32_t)c;  // (floor(log2 c) <= kPlanSub: the value itself)
   if (c > 0xFFFFFFFFull) return kPlanBuckets;
-  const uint32_t v = (uint32_t)c, l = 31 - __clz(v);  // floor(log2 c) >= 1
-  return min(2 * l + ((v >> (l - 1)) & 1u), kPlanBuckets - 1);
+  const uint32_t v = (uint32_t)c, l = 31 - __clz(v);  // floor(log2 c) > kPlanSub
+  return min((l << kPlanSub) + ((v >> (l - kPlanSub)) & ((1u << kPlanSub) - 1u)), kPlanBuckets - 1);
 }
+// sched words: [8, 8 + B) histogram, [8 + B, 8 + 2B) bucket offsets, [8 + 2B, 8 + 3B) cursors
+constexpr uint32_t kSchedHist = 8, kSchedOff = 8 + kPlanBuckets, kSchedCur = 8 + 2 * kPlanBuckets;
+static_assert(kSchedCur + kPlanBuckets <= kSchedWords, "sched buffer");
 // Both passes count in LDS first: a frame's tiles crowd a few buckets, and per-tile global atomics
 // on those few words serialize (0.3 ms per pass at 1080p).
 __global__ __launch_bounds__(256) void plan_hist(uint32_t* sched, const uint32_t* cost, uint32_t tiles) {
@@ -2812,12 +2821,12 @@ __global__ __launch_bounds__(256) void plan_hist(uint32_t* sched, const uint32_t
   __syncthreads();
   if (i < tiles) atomicAdd(&h[cost_bucket(cost[i])], 1u);
   __syncthreads();
-  if (threadIdx.x < kPlanBuckets && h[threadIdx.x]) atomicAdd(&sched[8 + threadIdx.x], h[threadIdx.x]);
+  if (threadIdx.x < kPlanBuckets && h[threadIdx.x]) atomicAdd(&sched[kSchedHist + threadIdx.x], h[threadIdx.x]);
 }
 // Items of a heavy tile in bucket b >= hb: doubling per octave above the threshold (costs [1, 2) x
 // threshold: 2 items, [2, 4): 4, ... up to 64 single pixels), at most kmax; kmax = 1: never split.
 __device__ __forceinline__ uint32_t bucket_items(uint32_t b, uint32_t hb, uint32_t kmax) {
-  return b < hb ? 1u : min(kmax, 2u << min((b - hb) >> 1, 5u));
+  return b < hb ? 1u : min(kmax, 2u << min((b - hb) >> kPlanSub, 5u));
 }
 __global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves, uint32_t factor, uint32_t kmax,
                                                 uint32_t prio) {
@@ -2826,8 +2835,8 @@ __global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves,
   const uint32_t hb = cost_bucket((unsigned long long)factor * sum / (waves ? waves : 1u));
   uint32_t pos = 0, heavy = 0, heavy_items = 0;
   for (int b = (int)kPlanBuckets - 1; b >= 0; --b) {
-    const uint32_t cnt = sched[8 + b], hv = (uint32_t)b >= hb, k = bucket_items((uint32_t)b, hb, kmax);
-    sched[72 + b] = pos;
+    const uint32_t cnt = sched[kSchedHist + b], hv = (uint32_t)b >= hb, k = bucket_items((uint32_t)b, hb, kmax);
+    sched[kSchedOff + b] = pos;
     pos += cnt * k;
     heavy += hv ? cnt : 0u;
     heavy_items += hv ? cnt * k : 0u;
@@ -2852,7 +2861,7 @@ __global__ __launch_bounds__(256) void plan_fill(uint32_t* sched, const uint32_t
   const uint32_t local = i < tiles ? atomicAdd(&cnt[b], k) : 0u;
   __syncthreads();
   if (threadIdx.x < kPlanBuckets && cnt[threadIdx.x])
-    base[threadIdx.x] = sched[72 + threadIdx.x] + atomicAdd(&sched[136 + threadIdx.x], cnt[threadIdx.x]);
+    base[threadIdx.x] = sched[kSchedOff + threadIdx.x] + atomicAdd(&sched[kSchedCur + threadIdx.x], cnt[threadIdx.x]);
   __syncthreads();
   if (i >= tiles) return;
   const uint32_t at = base[b] + local;
@@ -3406,7 +3415,7 @@ static hipError_t prepare_schedule(TraceParams& q, hipStream_t stream) {
   q.items = plan ? q.item_buf : nullptr;
   hipError_t e;
   if (plan) {
-    if ((e = hipMemsetAsync(q.sched + 8, 0, 192 * 4, stream)) != hipSuccess) return e;  // histogram, cursors
+    if ((e = hipMemsetAsync(q.sched + kSchedHist, 0, 3 * kPlanBuckets * 4, stream)) != hipSuccess) return e;  // histogram, cursors
     plan_hist<<<(tiles + 255) / 256, 256, 0, stream>>>(q.sched, q.tile_cost, tiles);
     // factor auto (-1): 3 when a resident wave gets more than 4 tiles, else 1 (profiles/r01k_schedule_sweep)
     // a launch of nf frames: a resident wave's fair share is nf frames' work, i.e. waves / nf per frame
