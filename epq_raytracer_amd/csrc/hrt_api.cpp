@@ -249,6 +249,32 @@ extern "C" hrt_status hrt_debug_check_guards(hrt_context* ctx, uint32_t* buffers
 #endif
 }
 
+// Test support: the context's grazing-band structure as the device holds it -- the per-cell records
+// (band_records), the offsets and the entry words -- so a test can hold the device-built records to the
+// lists they summarise.  info = {cells, entries, wide (32-bit entries), records present}.
+extern "C" hrt_status hrt_debug_band_records(hrt_context* ctx, uint32_t* rec, uint64_t rec_words, uint32_t* off,
+                                             uint64_t off_words, uint32_t* list_words, uint64_t list_cap,
+                                             uint32_t info[4]) {
+  if (!ctx || !info) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = hrt_synchronize(ctx);
+  if (st != HRT_OK) return st;
+  const hrt::SceneBufs& s = ctx->scene;
+  const uint64_t cells = s.bvh_band_off ? 6ull * s.bvh_dir_res * s.bvh_dir_res : 0ull;
+  const uint64_t entries = s.bvh_info[HRT_SCENE_BVH_BAND_ENTRIES];
+  const uint64_t words = s.bvh_band_wide ? entries : (entries + 1) / 2;
+  info[0] = (uint32_t)cells;
+  info[1] = (uint32_t)entries;
+  info[2] = s.bvh_band_wide;
+  info[3] = s.bvh_band_rec ? 1u : 0u;
+  if (rec && s.bvh_band_rec && rec_words >= cells * 8)
+    HRT_HIP(ctx, hipMemcpy(rec, s.bvh_band_rec, cells * 32, hipMemcpyDeviceToHost));
+  if (off && s.bvh_band_off && off_words >= cells + 1)
+    HRT_HIP(ctx, hipMemcpy(off, s.bvh_band_off, (cells + 1) * 4, hipMemcpyDeviceToHost));
+  if (list_words && s.bvh_band && list_cap >= words && words)
+    HRT_HIP(ctx, hipMemcpy(list_words, s.bvh_band, words * 4, hipMemcpyDeviceToHost));
+  return HRT_OK;
+}
+
 #ifndef HRT_BUILD_ID
 #define HRT_BUILD_ID "unknown"
 #endif

@@ -1405,6 +1405,7 @@ __device__ __forceinline__ void world_hit_bounce_bvh(const Scene& sc, const Trac
   if (sec && mask) {
     const uint32_t cell = dir_cell(d, P.bvh_dir_res);
     const uint32_t b0 = P.bvh_band_off[cell], b1 = P.bvh_band_off[cell + 1];
+    if (D && P.diag) dg.band_len += b1 - b0;  // (the same sum as BUNDLE_WQ's, which reads the cell records)
     // Pre-check: an entry whose d.n^ is outside (-tau_g - 2e-5, 3e-5) is not in this lane's band
     // (-tau_g - 1e-5, 2e-5).
     const BandCheck bc(d, -P.bvh_band_tau - 2e-5f, 3e-5f);

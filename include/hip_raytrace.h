@@ -513,6 +513,13 @@ hrt_status hrt_debug_band_flatten(int device, const uint32_t n[64], const uint32
 hrt_status hrt_debug_wq_protocol(int device, uint32_t rounds, const uint32_t* cnt, const uint32_t* take,
                                  const uint32_t* tgt, const uint64_t* val, const uint64_t seed[64], uint32_t* popped,
                                  uint64_t* seen, uint64_t slots[64], uint32_t* depth);
+/* Test support: the context's grazing-band structure as the device holds it (hrt_set_scene): the 32 B
+ * per-cell records of BUNDLE_WQ (8 words: list start, length, first 12 entries as half-words; rec_words >=
+ * 8 x cells), the offsets (off_words >= cells + 1) and the entry words (16-bit entries two to a word unless
+ * wide; list_cap >= the words).  A NULL or too small buffer is skipped.  info = {cells, entries, wide,
+ * records present}. */
+hrt_status hrt_debug_band_records(hrt_context* ctx, uint32_t* rec, uint64_t rec_words, uint32_t* off, uint64_t off_words,
+                                  uint32_t* list_words, uint64_t list_cap, uint32_t info[4]);
 /* HRT_TIMELINE builds: the last trace launch's item records (4 words each: start, tile list built, end,
  * item | frame << 32 | run << 40 | sky << 47 | wave << 48), at most cap of them copied; *count = the records the launch wrote (<= the
  * HRT_DEBUG_OPT_TIMELINE capacity).  Other builds: HRT_ERR_INVALID_ARGUMENT. */

@@ -653,3 +653,57 @@ def test_wq_handoff_protocol_matches_host(case):
     assert (seen[m] <= hi[m]).all(), "a slot read missed an earlier round's lowering"
     assert (seen[m] >= lo[m]).all(), "a slot read below the slot's value after its round"
     assert np.array_equal(slots, want_slots)
+
+
+@pytest.mark.parametrize("scene", ["island", "cave"])
+def test_band_records_match_the_lists(scene):
+    """The per-cell band records BUNDLE_WQ reads (r06: one 32 B record per direction cell, built on the
+    device by band_records from the uploaded offsets and 16-bit lists): for every cell, the list's start
+    and length, its first 12 entries as half-words in order, and zeros past them.  Both scenes have cells
+    with more than 12 entries (the lanes then read the rest from the list)."""
+    import ctypes
+    case = SceneCase(scene, (16, 16), 1, 2)
+    ctx = case.context()
+    lib = ctx.lib
+    info = (ctypes.c_uint32 * 4)()
+    _lib.check(lib.hrt_debug_band_records(ctx.handle, None, 0, None, 0, None, 0, info), "band records", ctx.handle, lib)
+    cells, entries, wide, has_rec = list(info)
+    assert cells == 6 * 1024 * 1024 and entries > 0 and wide == 0 and has_rec == 1
+    rec = np.zeros(cells * 8, np.uint32)
+    off = np.zeros(cells + 1, np.uint32)
+    words = np.zeros((entries + 1) // 2, np.uint32)
+    P = ctypes.c_void_p
+    _lib.check(lib.hrt_debug_band_records(ctx.handle, P(rec.ctypes.data), rec.size, P(off.ctypes.data), off.size,
+                                          P(words.ctypes.data), words.size, info), "band records", ctx.handle, lib)
+    ctx.close()
+    lst = words.view(np.uint16)[:entries].astype(np.uint32)
+    rec = rec.reshape(cells, 8)
+    n = np.diff(off.astype(np.int64))
+    assert int(off[-1]) == entries and (n >= 0).all()
+    assert np.array_equal(rec[:, 0], off[:-1]) and np.array_equal(rec[:, 1].astype(np.int64), n)
+    assert (n > 12).any(), "no cell overflows its record: the list path is not exercised"
+    half = rec[:, 2:].copy().view(np.uint16).reshape(cells, 12).astype(np.int64)
+    for j in range(12):
+        has = n > j
+        idx = off[:-1].astype(np.int64) + j
+        want = np.where(has, lst[np.minimum(idx, entries - 1)], 0)
+        assert np.array_equal(half[:, j], want), f"entry {j}"
+
+
+@pytest.mark.parametrize("scene", ["cave", "island"])
+def test_band_lookups_agree_between_records_and_offsets(scene):
+    """BUNDLE_WQ finds a bounce lane's band list through its cell record, BUNDLE_BVH through the offsets:
+    the same bounce segments (the frames are byte-identical) must see the same list lengths, summed over
+    every bounce lane of the frame (HRT_DIAG_BAND_SCAN_LEN).  r06: a build that cut lists at the record's
+    12 entries passed every frame test -- a band entry decides a hit only in rounding-noise cases -- so
+    the lookup is held here directly."""
+    case = SceneCase(scene, (96, 64), 4, 8)
+    sums = {}
+    for variant in (6, 9):  # BUNDLE_BVH, BUNDLE_WQ
+        ctx = case.context(variant=variant)
+        ctx.set_option(_lib.OPT_COUNTERS, 2)
+        ctx.trace(case.push(3))
+        sums[variant] = ctx.diagnostics()["band_scan_len"]
+        assert ctx.stats().last_kernel == variant
+        ctx.close()
+    assert sums[9] == sums[6] > 0, sums
