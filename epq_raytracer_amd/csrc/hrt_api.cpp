@@ -565,14 +565,22 @@ hrt_status build_scene(hrt_context* ctx, hrt::SceneBufs& s, const hrt_ray* rays,
         (st = up(s.bvh_keybase, bvh.key_base, "bvh key bases")) != HRT_OK)
       return st;
     // BUNDLE_WQ's per-cell band records (hrt_kernels.hip band_cell), built on the device from the lists
-    // just uploaded: one 32 B record per direction cell (6 x 1,024^2 cells: 201 MB), 16-bit lists only
+    // just uploaded: one 32 B record per direction cell (6 x 1,024^2 cells: 201 MB), 16-bit lists only.
+    // They only save memory traffic: where they do not fit, the lookups read the offsets and lists (the
+    // same bytes, tests/test_gpu_boundary.py::test_failed_set_scene_keeps_the_previous_scene).
     const size_t cells = bvh.band_off.empty() ? 0 : bvh.band_off.size() - 1;
     if (!bvh.band_wide() && cells) {
       hipError_t e = alloc((void**)&s.bvh_band_rec, cells * 32);
-      if (e == hipSuccess)
+      if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();  // (not a sticky error)
+        s.bvh_band_rec = nullptr;
+      } else if (e == hipSuccess) {
         e = hrt::launch_band_records(s.bvh_band_off, static_cast<const uint32_t*>(s.bvh_band), s.bvh_band_rec,
                                      (uint32_t)cells, ctx->stream);
-      if (e != hipSuccess) return hip_fail(ctx, e, "hrt_set_scene: band records");
+        if (e != hipSuccess) return hip_fail(ctx, e, "hrt_set_scene: band records");
+      } else {
+        return hip_fail(ctx, e, "hrt_set_scene: hipMalloc(band records)");
+      }
     }
   }
   s.bvh_info[HRT_SCENE_BVH_NODES] = bvh.n_nodes;

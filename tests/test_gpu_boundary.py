@@ -289,23 +289,39 @@ def test_failed_set_scene_keeps_the_previous_scene():
     """a failure inside hrt_set_scene (here the k-th device allocation, injected through
     libhip_raytrace_debug.so) must not leave stale counts next to freed buffers: the call reports
     HRT_ERR_OUT_OF_MEMORY and the previous scene still traces byte for byte."""
+    import ctypes
     box = SceneCase("box", (48, 40), 2, 4)
     island = SceneCase("island", (48, 40), 2, 8)
     ref = box.oracle()[0]
+    island_ref = island.oracle()[0]
     ctx = E.HrtContext(box.size, device=0, debug=True)
     ctx.set_scene(box.rays, box.spheres, box.tris, box.meshes)
-    k = 1
+    k, records_fallback = 1, False
     while True:
         ctx.set_option(_lib.DEBUG_OPT_FAIL_ALLOC, k)
         try:
             ctx.set_scene(island.rays, island.spheres, island.tris, island.meshes)
-            break  # fewer than k allocations: the injection did not fire, the scene is island now
         except _lib.HrtError as e:
             assert "OUT_OF_MEMORY" in str(e), e
-        ctx.trace(box.push())
-        assert np.array_equal(ctx.read(_lib.IMG_TRACE), ref), f"allocation {k}"
-        k += 1
-    assert k > 10  # rays, records, camera lists of both lanes, hierarchy, band lists ...
+            ctx.trace(box.push())
+            assert np.array_equal(ctx.read(_lib.IMG_TRACE), ref), f"allocation {k}"
+            k += 1
+            continue
+        info = (ctypes.c_uint32 * 4)()
+        _lib.check(ctx.lib.hrt_debug_band_records(ctx.handle, None, 0, None, 0, None, 0, info), "records",
+                   ctx.handle, ctx.lib)
+        if info[0] and not info[3]:
+            # the k-th allocation was the band records' (r06): the scene is set without them and the
+            # band lookups read the offsets and lists -- the same frame
+            records_fallback = True
+            ctx.trace(island.push())
+            assert np.array_equal(ctx.read(_lib.IMG_TRACE), island_ref), "without band records"
+            ctx.set_option(_lib.DEBUG_OPT_FAIL_ALLOC, 0)
+            ctx.set_scene(box.rays, box.spheres, box.tris, box.meshes)
+            k += 1
+            continue
+        break  # fewer than k allocations: the injection did not fire, the scene is island now
+    assert k > 10 and records_fallback  # rays, records, camera lists of both lanes, hierarchy, band lists ...
     ctx.trace(island.push())
     assert np.array_equal(ctx.read(_lib.IMG_TRACE), island.oracle()[0])
     n, bad = ctx.check_guards()
