@@ -129,7 +129,7 @@ EXPORTED_SYMBOLS = (
     "hrt_read_image", "hrt_load_accumulator", "hrt_get_layout", "hrt_synchronize", "hrt_get_stats", "hrt_reset_stats", "hrt_set_option",
     "hrt_get_diagnostics", "hrt_get_tile_profile", "hrt_get_scene_info", "hrt_generate_rays", "hrt_read_rays",
     "hrt_import_external_memory", "hrt_release_external_memory", "hrt_debug_export_memory", "hrt_debug_unmap_memory", "hrt_debug_math_check", "hrt_debug_math_check_rng", "hrt_debug_band_flatten", "hrt_debug_wq_protocol",
-    "hrt_debug_timeline", "hrt_debug_band_records",
+    "hrt_debug_timeline", "hrt_debug_band_records", "hrt_debug_tile_costs",
     "hrt_stream", "hrt_release_caches", "hrt_last_error", "hrt_comm_unique_id", "hrt_comm_init", "hrt_comm_init_all", "hrt_comm_info",
     "hrt_host_create_rays", "hrt_host_ray_grid", "hrt_host_view_matrix", "hrt_host_transform_meshes",
     "hrt_debug_bvh_build", "hrt_debug_bvh_wq_nodes",
@@ -202,6 +202,7 @@ def load(debug: bool = False) -> ctypes.CDLL:
         "hrt_debug_wq_protocol": (c_int32, [c_int32, c_uint32, P, P, P, P, P, P, P, P, P]),
         "hrt_debug_timeline": (c_int32, [c_void_p, P, c_uint32, P]),
         "hrt_debug_band_records": (c_int32, [c_void_p, P, c_uint64, P, c_uint64, P, c_uint64, P]),
+        "hrt_debug_tile_costs": (c_int32, [c_void_p, P, c_uint32]),
         "hrt_debug_bvh_build": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, P, c_uint64, P, c_uint64, P,
                                           c_uint64, P, c_uint64, P, c_uint64]),
         "hrt_debug_bvh_wq_nodes": (c_int64, [P, c_uint32, P, c_uint32, c_uint32, c_uint32, P, c_uint64]),

@@ -249,6 +249,18 @@ extern "C" hrt_status hrt_debug_check_guards(hrt_context* ctx, uint32_t* buffers
 #endif
 }
 
+// Tuning support: lane 0's per-tile costs as the last persistent launch on it recorded them (the next
+// launch's plan input; shader clocks / 16 per 8x8 tile, summed over the launch's frames).
+extern "C" hrt_status hrt_debug_tile_costs(hrt_context* ctx, uint32_t* out, uint32_t count) {
+  if (!ctx || !out) return HRT_ERR_INVALID_ARGUMENT;
+  hrt_status st = hrt_synchronize(ctx);
+  if (st != HRT_OK) return st;
+  if (!ctx->lane[0].tile_cost) return fail(ctx, HRT_ERR_INVALID_ARGUMENT, "hrt_debug_tile_costs: no trace yet");
+  const uint32_t n = std::min(count, (uint32_t)ctx->num_tiles());
+  HRT_HIP(ctx, hipMemcpy(out, ctx->lane[0].tile_cost, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return HRT_OK;
+}
+
 // Test support: the context's grazing-band structure as the device holds it -- the per-cell records
 // (band_records), the offsets and the entry words -- so a test can hold the device-built records to the
 // lists they summarise.  info = {cells, entries, wide (32-bit entries), records present}.

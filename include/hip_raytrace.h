@@ -520,6 +520,9 @@ hrt_status hrt_debug_wq_protocol(int device, uint32_t rounds, const uint32_t* cn
  * records present}. */
 hrt_status hrt_debug_band_records(hrt_context* ctx, uint32_t* rec, uint64_t rec_words, uint32_t* off, uint64_t off_words,
                                   uint32_t* list_words, uint64_t list_cap, uint32_t info[4]);
+/* Tuning support: trace lane 0's per-8x8-tile costs as the last persistent launch on it recorded them
+ * (shader clocks / 16 summed over the launch's frames; the next launch's plan input), count <= tiles. */
+hrt_status hrt_debug_tile_costs(hrt_context* ctx, uint32_t* out, uint32_t count);
 /* HRT_TIMELINE builds: the last trace launch's item records (4 words each: start, tile list built, end,
  * item | frame << 32 | run << 40 | sky << 47 | wave << 48), at most cap of them copied; *count = the records the launch wrote (<= the
  * HRT_DEBUG_OPT_TIMELINE capacity).  Other builds: HRT_ERR_INVALID_ARGUMENT. */

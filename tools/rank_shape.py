@@ -36,6 +36,16 @@ def run(args, part):
         ctx.set_option(k, v)
     raytrace.init()
     diffuse.next_frame(0, raytrace.image())
+    if args.burn_ms > 0:  # (diagnosis) other GPU work right before the warm-up: does the clock ramp matter?
+        burn = E.HrtContext((W, H), device=0, mode=_lib.MODE_RGBA8)
+        brt = E.RayTracePipeline(burn, (W, H), settings)
+        t_end = time.perf_counter() + args.burn_ms / 1e3
+        k = 1
+        while time.perf_counter() < t_end:
+            burn.compute_n(brt.push_constants(camera, k, False), 4)
+            burn.synchronize()
+            k += 4
+        burn.close()
     ctx.compute_n(raytrace.push_constants(camera, 1, False), args.warmup)
     ctx.synchronize()
     ctx.reset_stats()
@@ -60,6 +70,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--burn-ms", type=float, default=0.0, help="(diagnosis) GPU matmul work before each warm-up")
     ap.add_argument("--parts", type=int, nargs="*", default=None, help="partition indices (default all)")
     ap.add_argument("--option", type=lambda s: tuple(int(v) for v in s.split("=")), action="append", default=[],
                     help="KEY=VALUE hrt_set_option before the scene (repeatable)")

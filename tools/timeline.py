@@ -122,6 +122,7 @@ def main():
     ap.add_argument("--option", type=lambda s: tuple(int(v) for v in s.split("=")), action="append", default=[])
     ap.add_argument("--json", default=None)
     ap.add_argument("--raw", default=None, help="also save the raw records (.npy)")
+    ap.add_argument("--costs", default=None, help="save the warm-up launch's per-tile costs (.npy)")
     a = ap.parse_args()
     W, H = a.width, a.height
     camera, settings = E.preset(a.scene)
@@ -137,6 +138,11 @@ def main():
     raytrace.init()
     diffuse.next_frame(0, raytrace.image())
     ctx.compute_n(raytrace.push_constants(camera, 1, False), a.warmup)
+    if a.costs:  # the warm-up's per-tile costs: the timed launch's plan input
+        costs = np.zeros(ctx.local_rows // 8 * ((W + 7) // 8) + 64, np.uint32)
+        _lib.check(ctx.lib.hrt_debug_tile_costs(ctx.handle, _lib.ptr(costs), costs.size), "tile costs", ctx.handle,
+                   ctx.lib)
+        np.save(a.costs, costs)
     ctx.synchronize()
     ctx.reset_stats()
     ctx.compute_n(raytrace.push_constants(camera, 1 + a.warmup, False), a.steps)
