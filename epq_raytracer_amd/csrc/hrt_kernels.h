@@ -91,6 +91,7 @@ struct TraceParams {
   // per lane, n, ok, aabb lo / hi, aabb_ok), filled by the tile_lists kernel before the trace; nullptr = off
   uint32_t* tl_cache;
   uint32_t tl_lists_ready;  // tl_cache already holds this camera's lists (hrt_api.cpp launch_frames): no tile_lists
+  uint32_t split_factor4;   // (host side, launch_trace) the heavy threshold in quarters of a wave's share; 0: split_factor
 };
 constexpr uint32_t kTlRecWords = 136;
 

@@ -2829,11 +2829,12 @@ __global__ __launch_bounds__(256) void plan_hist(uint32_t* sched, const uint32_t
 __device__ __forceinline__ uint32_t bucket_items(uint32_t b, uint32_t hb, uint32_t kmax) {
   return b < hb ? 1u : min(kmax, 2u << min((b - hb) >> kPlanSub, 5u));
 }
-__global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves, uint32_t factor, uint32_t kmax,
+// factor4: the heavy threshold in quarters of a resident wave's share of the launch's work
+__global__ __launch_bounds__(64) void plan_scan(uint32_t* sched, uint32_t waves, uint32_t factor4, uint32_t kmax,
                                                 uint32_t prio) {
   if (threadIdx.x != 0) return;
   const unsigned long long sum = *reinterpret_cast<const unsigned long long*>(sched + 6);
-  const uint32_t hb = cost_bucket((unsigned long long)factor * sum / (waves ? waves : 1u));
+  const uint32_t hb = cost_bucket((unsigned long long)factor4 * sum / (4ull * (waves ? waves : 1u)));
   uint32_t pos = 0, heavy = 0, heavy_items = 0;
   for (int b = (int)kPlanBuckets - 1; b >= 0; --b) {
     const uint32_t cnt = sched[kSchedHist + b], hv = (uint32_t)b >= hb, k = bucket_items((uint32_t)b, hb, kmax);
@@ -3422,8 +3423,9 @@ static hipError_t prepare_schedule(TraceParams& q, hipStream_t stream) {
     // a launch of nf frames: a resident wave's fair share is nf frames' work, i.e. waves / nf per frame
     const uint32_t nf = q.n_frames > 1 ? q.n_frames : 1u;
     const uint32_t waves = std::max(1u, q.num_cus * 16u / nf);
-    const uint32_t factor = q.split_factor >= 0 ? (uint32_t)q.split_factor : tiles > 4 * waves ? 3u : 1u;
-    plan_scan<<<1, 64, 0, stream>>>(q.sched, waves, factor, q.split_k, q.split_prio);
+    const uint32_t factor4 =
+        q.split_factor4 ? q.split_factor4 : 4u * (q.split_factor >= 0 ? (uint32_t)q.split_factor : tiles > 4 * waves ? 3u : 1u);
+    plan_scan<<<1, 64, 0, stream>>>(q.sched, waves, factor4, q.split_k, q.split_prio);
     plan_fill<<<(tiles + 255) / 256, 256, 0, stream>>>(q.sched, q.tile_cost, tiles, q.split_k, q.split_prio,
                                                        q.item_buf);
   }
@@ -3513,7 +3515,13 @@ hipError_t launch_trace(const TraceParams& p0, int variant, hipStream_t stream, 
       // resident wave gets more than 6 tiles (the full frame), else 3 (row partitions at N > 1)
       // (profiles/r01o_lane_weighted_sum_factor_sweep.jsonl)
       if (q.split_k == 0) q.split_k = 8;
-      if (q.split_factor < 0)
+      // A launch of several frames (hrt_compute_n) splits a tile from 1.25 x a wave's share of the launch:
+      // a rank of 8 holds 1/8 of the rows but the same pixel chains, and one cave tile's frame took 18 ms
+      // against a 15 ms share, unsplit at 2 x (profiles/r06/r06aa/).  Cave's slowest rank of 8 0.88 ->
+      // 0.80 ms per frame; island, 2 and 4 ranks and whole frames within noise (r06ac, r06ad).
+      if (q.split_factor < 0 && p.n_frames > 1)
+        q.split_factor4 = 5;
+      else if (q.split_factor < 0)
         q.split_factor = (uint64_t)tiles_of(p) * std::max(1u, p.n_frames) > 6ull * p.num_cus * 16u ? 2 : 3;
       const size_t lds = wq_lds_bytes(p, &q.wq_ncap, &q.wq_tcap);
       if (p.wq_ncap) q.wq_ncap = std::min(q.wq_ncap, std::max(128u, p.wq_ncap & ~63u));  // HRT_OPT_WQ_NODE_CAP

@@ -244,8 +244,9 @@ typedef enum hrt_option {
    * threshold.  The frame's time is set by its slowest tiles' sample chains; results do not depend on it. */
   HRT_OPT_SPLIT = 5,
   /* heavy tile: its cost in the previous trace exceeds this multiple of a resident wave's fair share
-   * (sum of tile costs / resident waves), to a half octave (0: every tile is heavy; default -1 =
-   * auto: BUNDLE_WQ 2; the others 3 when there are more than 4 tiles per resident wave, else 1) */
+   * (sum of tile costs / resident waves), to an eighth octave (0: every tile is heavy; default -1 =
+   * auto: BUNDLE_WQ 1.25 in a launch of several frames (hrt_compute_n), else 2 (3 when a resident
+   * wave gets at most 6 tiles); the others 3 when there are more than 4 tiles per resident wave, else 1) */
   HRT_OPT_SPLIT_FACTOR = 6,
   /* persistent kernels: heavy tiles (as above) run at raised wave issue priority (1 default, 0 off;
    * libhip_raytrace_debug.so only: 2 = a planned trace runs ONLY the heavy tiles, the frame is
