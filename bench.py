@@ -301,7 +301,7 @@ def main():
     last_trace = ctx.read(_lib.IMG_TRACE, _lib.FMT_RGBA8) if world == 1 else None
     gathered = full.cpu().numpy() if (dist_on and rank == 0 and full is not None) else None
     # the realtime loop (compute_then_render per frame, src/main.rs:41-57): consecutive traces overlap
-    # on the context's two trace lanes; measured after the timed steps, separately reported
+    # on the context's trace lanes (three by default); measured after the timed steps, separately reported
     rt_ms = None
     if args.realtime_frames > 0 and fpl > 1:
         saved = fpl
