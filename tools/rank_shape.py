@@ -90,12 +90,12 @@ def main():
     # An N-GPU step waits for its slowest rank IN THAT RUN: per round, the slowest
     # part against that round's whole frame / N; the summary is the worst round, not each part's best.
     runs = []
-    for r in range(a.rounds):
+    for r in range(a.rounds if parts else 0):  # (--parts with no values: whole frames only)
         fair_r = whole[r] / a.gpus
         slow_r = max(parts, key=lambda p: per[p][r])
         runs.append({"round": r, "fair_share_ms": round(fair_r, 4), "slowest_part": slow_r,
                      "slowest_ms": round(per[slow_r][r], 4), "slowest_over_fair": round(per[slow_r][r] / fair_r, 4)})
-    worst = max(runs, key=lambda x: x["slowest_over_fair"])
+    worst = max(runs, key=lambda x: x["slowest_over_fair"]) if runs else {"slowest_over_fair": None}
     print(json.dumps({"summary": True, "scene": a.scene, "gpus": a.gpus, "shape": f"{a.warmup} warm-up + {a.steps}",
                       "whole_kernel_ms": [round(v, 4) for v in whole],
                       "part_kernel_ms": {p: [round(v, 4) for v in per[p]] for p in parts},
