@@ -706,6 +706,27 @@ def test_band_records_match_the_lists(scene):
         assert np.array_equal(half[:, j], want), f"entry {j}"
 
 
+def test_tile_costs_cover_every_tile_of_the_last_launch():
+    """hrt_debug_tile_costs (the planner's input, read by tools/timeline.py --costs): after a multi-frame
+    persistent launch every 8x8 tile of the frame carries a cost (shader clocks / 16 summed over the
+    launch's frames), and nothing is written past the frame's tiles."""
+    import ctypes
+    W, H = 64, 48
+    tiles = (W // 8) * (H // 8)
+    case = SceneCase("island", (W, H), 2, 3)
+    ctx = case.context()
+    ctx.trace(case.push(init=True))
+    ctx.accumulate(0)
+    ctx.compute_n(case.push(1), 4)
+    assert ctx.stats().last_kernel == _lib.KERNEL_BUNDLE_WQ, "the persistent BUNDLE_WQ kernel records tile costs"
+    costs = np.zeros(tiles + 16, np.uint32)
+    _lib.check(ctx.lib.hrt_debug_tile_costs(ctx.handle, ctypes.c_void_p(costs.ctypes.data), costs.size),
+               "tile costs", ctx.handle, ctx.lib)
+    ctx.close()
+    assert (costs[:tiles] > 0).all(), costs[:tiles]
+    assert (costs[tiles:] == 0).all()
+
+
 @pytest.mark.parametrize("scene", ["cave", "island"])
 def test_band_lookups_agree_between_records_and_offsets(scene):
     """BUNDLE_WQ finds a bounce lane's band list through its cell record, BUNDLE_BVH through the offsets:
